@@ -1,0 +1,138 @@
+"""airs-compression_amd -- MI355X-native AIRSPACE encode path.
+
+Python side of the drop-in: ctypes bindings over ``lib/libairscmp.so``
+(built from ``csrc/`` by the Makefile).  ``cmpapi`` mirrors the reference's
+lib/cmp.h API; :class:`GpuEngine` binds the device batch API of
+include/cmp_gpu.h.  The library has no CPU encode path: compress calls need
+the HIP device, and loading fails loudly when the shared object is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_int, c_uint32, c_uint64, c_void_p
+
+from .cmpapi import *  # noqa: F401,F403
+from .cmpapi import CmpContext, CmpLib, is_error, error_name
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libairscmp.so")
+
+GPU_U16, GPU_I16, GPU_I16_IN_I32 = 0, 1, 2
+GPU_AUTO_RICE = 0x1
+KIND_TO_GPU = {"u16": GPU_U16, "i16": GPU_I16, "i16_in_i32": GPU_I16_IN_I32}
+
+
+def build(jobs: int = 8) -> str:
+    """Compile csrc/ into lib/libairscmp.so (hipcc for gfx950 + gcc)."""
+    subprocess.run(["make", f"-j{jobs}", "-C", PKG_DIR], check=True)
+    return LIB_PATH
+
+
+def _one_hip_runtime() -> None:
+    """PyTorch-ROCm ships its own libamdhip64.so (SONAME libamdhip64.so.7, the
+    same as /opt/rocm's).  If libairscmp.so were dlopen'ed first, torch would
+    later map a second HIP runtime into the process and fail to see the GPU.
+    Importing torch first makes the library bind to torch's copy, so device
+    pointers, streams and events are shared.  Without torch the library uses
+    /opt/rocm's runtime as usual."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
+def load(path: str | None = None) -> "AirsLib":
+    path = path or LIB_PATH
+    _one_hip_runtime()
+    if not os.path.exists(path):
+        raise FileNotFoundError(
+            f"{path} is missing: build it with `make -C {PKG_DIR}` (no CPU fallback exists)")
+    return AirsLib(path)
+
+
+class GpuBatch(ctypes.Structure):
+    """struct cmp_gpu_batch (include/cmp_gpu.h)."""
+    _fields_ = [
+        ("type", c_int),
+        ("src", c_void_p),
+        ("src_stride", c_uint64),
+        ("src_size", c_uint32),
+        ("dst", c_void_p),
+        ("dst_stride", c_uint64),
+        ("dst_capacity", c_uint32),
+        ("sizes", c_void_p),
+        ("flags", c_uint32),
+    ]
+
+
+class AirsLib(CmpLib):
+    """CmpLib plus the cmp_gpu.h device batch API."""
+
+    def __init__(self, path: str = LIB_PATH):
+        super().__init__(path)
+        L = self.lib
+        L.cmp_gpu_available.restype = c_int
+        L.cmp_gpu_engine_create.argtypes = [POINTER(c_void_p), c_void_p]
+        L.cmp_gpu_engine_create.restype = c_uint32
+        L.cmp_gpu_engine_destroy.argtypes = [c_void_p]
+        L.cmp_gpu_engine_destroy.restype = None
+        L.cmp_gpu_compress.argtypes = [c_void_p, POINTER(CmpContext), c_uint32, c_uint32, POINTER(GpuBatch)]
+        L.cmp_gpu_compress.restype = c_uint32
+        L.cmp_gpu_synchronize.argtypes = [c_void_p]
+        L.cmp_gpu_synchronize.restype = c_uint32
+        L.cmp_gpu_synthesize.argtypes = [c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_uint32,
+                                         c_uint32, c_uint64, c_uint32]
+        L.cmp_gpu_synthesize.restype = c_uint32
+
+    def gpu_available(self) -> bool:
+        return bool(self.lib.cmp_gpu_available())
+
+    def engine(self, stream: int | None = None) -> "GpuEngine":
+        return GpuEngine(self, stream)
+
+
+class GpuEngine:
+    """One cmp_gpu_engine bound to a HIP stream (raw hipStream_t handle)."""
+
+    def __init__(self, lib: AirsLib, stream: int | None = None):
+        self.lib = lib
+        h = c_void_p()
+        r = lib.lib.cmp_gpu_engine_create(ctypes.byref(h), stream)
+        if is_error(r):
+            raise RuntimeError(f"cmp_gpu_engine_create failed: {error_name(r)}")
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self.lib.lib.cmp_gpu_engine_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compress(self, ctxs, frames_per_ctx: int, kind: str, src_ptr: int, src_stride: int,
+                 src_size: int, dst_ptr: int, dst_stride: int, dst_capacity: int, sizes_ptr: int,
+                 flags: int = 0) -> int:
+        """cmp_gpu_compress over device pointers; ctxs is a ctypes CmpContext array."""
+        b = GpuBatch(type=KIND_TO_GPU[kind], src=src_ptr, src_stride=src_stride, src_size=src_size,
+                     dst=dst_ptr, dst_stride=dst_stride, dst_capacity=dst_capacity,
+                     sizes=sizes_ptr, flags=flags)
+        n_ctx = len(ctxs)
+        return self.lib.lib.cmp_gpu_compress(self.handle, ctxs, n_ctx, frames_per_ctx, ctypes.byref(b))
+
+    def synchronize(self) -> int:
+        return self.lib.lib.cmp_gpu_synchronize(self.handle)
+
+    def synthesize(self, dst_ptr: int, sample_bytes: int, seed: int, frame0: int, n: int,
+                   num_frames: int, stride: int, noise_w: int) -> int:
+        return self.lib.lib.cmp_gpu_synthesize(self.handle, dst_ptr, sample_bytes, seed, frame0, n,
+                                               num_frames, stride, noise_w)
+
+
+def context_array(n: int):
+    return (CmpContext * n)()

@@ -1,0 +1,126 @@
+/*
+ * airs_dev.h -- internal C-ABI between the C host library (cmp_host.c) and
+ * the HIP device layer (encode.hip).  Plain C types only.
+ *
+ * One launch encodes `num_frames` equally sized frames that share one set of
+ * pass parameters (the reference's compress_engine, lib/compress/cmp.c:213-338,
+ * run for many frames at once).  Per-frame variation (identifier, Golomb
+ * parameter, model buffer) comes through optional device arrays.
+ */
+#ifndef AIRS_DEV_H
+#define AIRS_DEV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum airs_model_mode {
+	AIRS_MODEL_NONE = 0,   /* no model configured */
+	AIRS_MODEL_STORE = 1,  /* primary pass: model[i] = sample[i]   (cmp.c:305-306) */
+	AIRS_MODEL_UPDATE = 2  /* secondary pass: model[i] = blend(...) (cmp.c:307-310) */
+};
+
+struct airs_launch {
+	/* input: frame f's samples at src + f*src_stride; 2 or 4 bytes per sample */
+	const void *src;
+	uint64_t src_stride;
+	uint32_t sample_bytes;   /* 2 (u16/i16) or 4 (i16 in i32) */
+	uint32_t is_unsigned;    /* u16: zero-extend in the model update (cmp.c:132-142) */
+	uint32_t n;              /* samples per frame, >= 1 */
+	uint32_t num_frames;
+	/* launch frame j is batch frame frame_list[j] (device, optional) or
+	 * frame_add + j*frame_mul; per-frame arrays below are indexed by the
+	 * batch frame, identifiers and model pointers by the launch index j */
+	const uint32_t *frame_list;
+	uint32_t frame_add, frame_mul;
+
+	/* output: frame f at dst + f*dst_stride (8-byte aligned), capacity cap */
+	void *dst;
+	uint64_t dst_stride;
+	uint32_t cap;
+
+	/* pass parameters (already validated by the host) */
+	uint32_t preprocessing;  /* enum cmp_preprocessing: NONE, DIFF or MODEL */
+	uint32_t encoder_type;   /* enum cmp_encoder_type */
+	uint32_t encoder_param;  /* Golomb g (ignored for UNCOMPRESSED) */
+	uint32_t outlier_param;  /* user outlier (GOLOMB_MULTI) */
+	const uint32_t *frame_g; /* device, optional per-frame g (all powers of two) */
+
+	/* model (work buffer): batch frame f's model at model + (f / model_div)*model_stride,
+	 * or model_ptrs[j] (device) */
+	void *model;
+	uint64_t model_stride;
+	uint32_t model_div;
+	const uint64_t *model_ptrs;
+	uint32_t model_mode;     /* enum airs_model_mode */
+	uint32_t model_rate;
+	uint64_t fail_bit;       /* samples reaching this frame bit keep their old model */
+
+	/* header fields */
+	uint64_t id_base;        /* identifier of launch frame j = id_base + j*id_step, or ids[j] */
+	uint64_t id_step;
+	const uint64_t *ids;     /* device, optional */
+	uint32_t seq;            /* sequence number written in the header */
+	uint32_t checksum_enabled;
+	const uint32_t *checksums; /* device, per frame (airs_dev_checksum output) */
+
+	/* results (device): status[f] = frame size or error value; needed[f] = size in
+	 * bytes the frame needs (payload+header+checksum), even when it did not fit */
+	uint32_t *status;
+	uint32_t *needed;
+};
+
+struct airs_dev_engine;
+
+/* create an engine on the current HIP device; stream = hipStream_t or NULL (default) */
+struct airs_dev_engine *airs_dev_engine_create(void *stream);
+void airs_dev_engine_destroy(struct airs_dev_engine *e);
+void *airs_dev_engine_stream(struct airs_dev_engine *e);
+
+/* enqueue one encode launch; returns 0 or a cmp error value (uint32_t)-code */
+uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L);
+
+/* XXH32 (seed 419764627) over each frame's samples as big-endian 16-bit words */
+uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
+			   uint32_t sample_bytes, uint32_t n, uint32_t num_frames,
+			   const uint32_t *frame_list, uint32_t *out);
+
+/* per-frame Rice parameter (build-defined rule): out_g[f] = 2^k */
+uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
+			      uint32_t sample_bytes, uint32_t n, uint32_t num_frames,
+			      uint32_t preprocessing, uint32_t *out_g);
+
+/* counter-hash synthetic frames (bench/test inputs) */
+uint32_t airs_dev_synth(struct airs_dev_engine *e, void *dst, uint32_t sample_bytes, uint64_t seed,
+			uint32_t frame0, uint32_t n, uint32_t num_frames, uint64_t stride,
+			uint32_t W);
+
+/* engine-owned scratch, grown on demand (stream ordered) */
+void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes);
+
+/* rewrite header bytes 8..13 (identifier) of launch frames whose status is
+ * not an error: frame j = frame_add + j*frame_mul, identifier ids[j] (device) */
+uint32_t airs_dev_patch_ids(struct airs_dev_engine *e, void *dst, uint64_t dst_stride, uint32_t num_frames,
+			    uint32_t frame_add, uint32_t frame_mul, const uint64_t *ids,
+			    const uint32_t *status);
+
+/* plain memory helpers on the engine stream */
+void *airs_dev_malloc(size_t bytes);
+void airs_dev_free(void *p);
+uint32_t airs_dev_h2d(struct airs_dev_engine *e, void *dst, const void *src, size_t bytes);
+uint32_t airs_dev_d2h(struct airs_dev_engine *e, void *dst, const void *src, size_t bytes);
+uint32_t airs_dev_sync(struct airs_dev_engine *e);
+uint32_t airs_dev_memset(struct airs_dev_engine *e, void *dst, int v, size_t bytes);
+
+/* non-zero when a HIP device is usable */
+int airs_dev_available(void);
+const char *airs_dev_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIRS_DEV_H */

@@ -1,0 +1,829 @@
+/*
+ * cmp_host.c -- host side of libairscmp.so: the cmp.h API (drop-in for the
+ * reference's lib/compress/cmp.c + lib/common/cmp_errors.c) and the cmp_gpu.h
+ * device batch API.  Parameter validation, the context state machine
+ * (primary/secondary passes, identifiers, fallback) and all error codes
+ * follow the reference exactly; the per-sample work is done by the HIP
+ * kernels in encode.hip through airs_dev.h.  There is no CPU encode path:
+ * without a usable GPU the compress calls fail with CMP_ERR_GENERIC and a
+ * message on stderr.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "cmp.h"
+#include "cmp_errors.h"
+#include "cmp_gpu.h"
+#include "airs_dev.h"
+
+#define ERRV(name) ((uint32_t)0u - (uint32_t)CMP_ERR_##name)
+#define CTX_MAGIC 34021395u      /* reference lib/compress/cmp.c:23 */
+#define EXT_HDR_SIZE 6u          /* reference lib/common/header_private.h:35-39 */
+#define HDR_MAX_SIZE (CMP_HDR_SIZE + EXT_HDR_SIZE)
+#define MAX_MODEL_RATE 16u
+
+static unsigned is_err(uint32_t v)
+{
+	return v > ERRV(MAX_CODE);
+}
+
+/* ---------------- identifiers (reference cmp.c:27-50, 438-449) ---------------- */
+static uint64_t g_counter;
+
+static void counter_timestamp(uint32_t *coarse, uint16_t *fine)
+{
+	*coarse = (uint32_t)(g_counter >> 16);
+	*fine = (uint16_t)g_counter;
+	g_counter++;
+}
+
+static void (*g_timestamp)(uint32_t *, uint16_t *) = counter_timestamp;
+
+void cmp_set_timestamp_func(void (*f)(uint32_t *coarse, uint16_t *fine))
+{
+	g_timestamp = f ? f : counter_timestamp;
+}
+
+static uint64_t next_identifier(void)
+{
+	uint32_t coarse = 0;
+	uint16_t fine = 0;
+
+	g_timestamp(&coarse, &fine);
+	return ((uint64_t)coarse << 16) | (uint64_t)fine;
+}
+
+/* ---------------- errors (reference lib/common/cmp_errors.c) ---------------- */
+unsigned int cmp_is_error(uint32_t code)
+{
+	return is_err(code);
+}
+
+enum cmp_error cmp_get_error_code(uint32_t code)
+{
+	if (!is_err(code))
+		return CMP_ERR_NO_ERROR;
+	return (enum cmp_error)(0u - code);
+}
+
+const char *cmp_get_error_string(enum cmp_error code)
+{
+	static const struct {
+		enum cmp_error code;
+		const char *text;
+	} table[] = {
+		{ CMP_ERR_NO_ERROR, "No error detected" },
+		{ CMP_ERR_GENERIC, "Error (generic)" },
+		{ CMP_ERR_PARAMS_INVALID, "Invalid compression parameters" },
+		{ CMP_ERR_DST_TOO_SMALL, "Destination buffer is too small to hold the content" },
+		{ CMP_ERR_DST_NULL, "Destination buffer pointer is NULL" },
+		{ CMP_ERR_DST_UNALIGNED, "Destination buffer pointer is unaligned" },
+		{ CMP_ERR_SRC_SIZE_WRONG, "Source buffer size is invalid" },
+		{ CMP_ERR_SRC_NULL, "Source buffer pointer is NULL" },
+		{ CMP_ERR_SRC_SIZE_MISMATCH,
+		  "Source data size changed using model preprocessing; not allowed until reset" },
+		{ CMP_ERR_WORK_BUF_TOO_SMALL, "Work buffer is too small" },
+		{ CMP_ERR_WORK_BUF_NULL, "Work buffer is NULL but required" },
+		{ CMP_ERR_WORK_BUF_UNALIGNED, "Work buffer is unaligned" },
+		{ CMP_ERR_HDR_CMP_SIZE_TOO_LARGE, "Compressed size exceeds header field limit" },
+		{ CMP_ERR_HDR_ORIGINAL_TOO_LARGE, "Original size exceeds header field limit" },
+		{ CMP_ERR_CONTEXT_INVALID, "Compression context uninitialised or corrupted" },
+		{ CMP_ERR_INT_HDR, "Internal header processing error" },
+		{ CMP_ERR_INT_ENCODER, "Internal data encoder error" },
+		{ CMP_ERR_INT_BITSTREAM, "Internal bitstream writer error" },
+	};
+	size_t i;
+
+	for (i = 0; i < sizeof(table) / sizeof(table[0]); i++)
+		if (table[i].code == code)
+			return table[i].text;
+	return "Unspecified error code";
+}
+
+const char *cmp_get_error_message(uint32_t code)
+{
+	return cmp_get_error_string(cmp_get_error_code(code));
+}
+
+/* ---------------- encoder parameters (reference encoder.c:63-233) ---------------- */
+static uint32_t floor_log2(uint32_t x)
+{
+	return 31u - (uint32_t)__builtin_clz(x);
+}
+
+/* validate (type, g, outlier) and resolve the outlier written to the header */
+static uint32_t coder_resolve(uint32_t type, uint32_t g, uint32_t outlier, uint32_t *resolved)
+{
+	uint32_t k, cutoff, limit;
+	uint64_t want;
+
+	if (resolved)
+		*resolved = 0;
+	if (type == CMP_ENCODER_UNCOMPRESSED)
+		return 0;
+	if (type != CMP_ENCODER_GOLOMB_ZERO && type != CMP_ENCODER_GOLOMB_MULTI)
+		return ERRV(PARAMS_INVALID);
+	if (g < 1u || g > 0xFFFFu)
+		return ERRV(PARAMS_INVALID);
+	k = floor_log2(g);
+	cutoff = (2u << k) - g;
+	limit = cutoff + (31u - k) * g; /* first value needing a > 32-bit codeword */
+	if (type == CMP_ENCODER_GOLOMB_MULTI)
+		limit = limit > 8u ? limit - 8u : 0u; /* 8 escape symbols for 16-bit samples */
+	want = type == CMP_ENCODER_GOLOMB_ZERO ? (uint64_t)cutoff + 16ull * g - 1ull : (uint64_t)outlier;
+	if (want > limit)
+		want = limit;
+	if (want == 0)
+		return ERRV(PARAMS_INVALID);
+	if (resolved)
+		*resolved = (uint32_t)want;
+	return 0;
+}
+
+/* 48 bits per sample worst case (reference encoder.c:381-386) */
+static uint64_t payload_bound(uint32_t size)
+{
+	uint64_t n = ((uint64_t)size * 8u + 15u) / 16u;
+
+	return (n * 48u + 7u) / 8u;
+}
+
+uint32_t cmp_compress_bound(uint32_t packed_size)
+{
+	uint64_t b;
+
+	if (packed_size > CMP_HDR_MAX_ORIGINAL_SIZE)
+		return ERRV(HDR_ORIGINAL_TOO_LARGE);
+	b = HDR_MAX_SIZE + CMP_CHECKSUM_SIZE + payload_bound(packed_size);
+	if (b > CMP_HDR_MAX_COMPRESSED_SIZE)
+		return ERRV(HDR_CMP_SIZE_TOO_LARGE);
+	return (uint32_t)b;
+}
+
+static uint32_t pre_work_size(uint32_t pre, uint32_t size, int *known)
+{
+	*known = 1;
+	if (pre == CMP_PREPROCESS_NONE || pre == CMP_PREPROCESS_DIFF)
+		return 0;
+	if (pre == CMP_PREPROCESS_IWT || pre == CMP_PREPROCESS_MODEL)
+		return (size + 1u) & ~1u;
+	*known = 0;
+	return 0;
+}
+
+uint32_t cmp_cal_work_buf_size(const struct cmp_params *params, uint32_t src_size)
+{
+	uint32_t a, b = 0;
+	int known;
+
+	if (!params)
+		return ERRV(GENERIC);
+	if (params->primary_preprocessing == CMP_PREPROCESS_MODEL)
+		return ERRV(PARAMS_INVALID);
+	a = pre_work_size(params->primary_preprocessing, src_size, &known);
+	if (!known)
+		return ERRV(PARAMS_INVALID);
+	if (params->secondary_iterations) {
+		b = pre_work_size(params->secondary_preprocessing, src_size, &known);
+		if (!known)
+			return ERRV(PARAMS_INVALID);
+	}
+	return a > b ? a : b;
+}
+
+static int model_needed(const struct cmp_params *p)
+{
+	return p->secondary_preprocessing == CMP_PREPROCESS_MODEL && p->secondary_iterations != 0;
+}
+
+uint32_t cmp_reset(struct cmp_context *ctx)
+{
+	if (!ctx)
+		return ERRV(GENERIC);
+	if (ctx->magic != CTX_MAGIC)
+		return ERRV(CONTEXT_INVALID);
+	ctx->sequence_number = 0;
+	ctx->identifier = next_identifier();
+	ctx->model_size = 0;
+	return ERRV(NO_ERROR);
+}
+
+void cmp_deinitialise(struct cmp_context *ctx)
+{
+	if (ctx)
+		memset(ctx, 0, sizeof(*ctx));
+}
+
+uint32_t cmp_initialise(struct cmp_context *ctx, const struct cmp_params *params, void *work_buf,
+			uint32_t work_buf_size)
+{
+	uint32_t e, need;
+
+	if (!ctx)
+		return ERRV(GENERIC);
+	cmp_deinitialise(ctx);
+	if (!params || is_err(work_buf_size))
+		return ERRV(GENERIC);
+	if (params->secondary_iterations >= (1u << CMP_HDR_BITS_SEQUENCE_NUMBER))
+		return ERRV(PARAMS_INVALID);
+	e = coder_resolve(params->primary_encoder_type, params->primary_encoder_param,
+			  params->primary_encoder_outlier, NULL);
+	if (is_err(e))
+		return e;
+	if (params->secondary_iterations) {
+		e = coder_resolve(params->secondary_encoder_type, params->secondary_encoder_param,
+				  params->secondary_encoder_outlier, NULL);
+		if (is_err(e))
+			return e;
+	}
+	if (model_needed(params) && params->model_rate > MAX_MODEL_RATE)
+		return ERRV(PARAMS_INVALID);
+	need = cmp_cal_work_buf_size(params, 2);
+	if (is_err(need))
+		return need;
+	if (need) {
+		if (!work_buf)
+			return ERRV(WORK_BUF_NULL);
+		if (!work_buf_size)
+			return ERRV(WORK_BUF_TOO_SMALL);
+		if ((uintptr_t)work_buf & 1u)
+			return ERRV(WORK_BUF_UNALIGNED);
+	}
+	ctx->params = *params;
+	ctx->work_buf = work_buf;
+	ctx->work_buf_size = work_buf_size;
+	ctx->magic = CTX_MAGIC;
+	return cmp_reset(ctx);
+}
+
+/* ================================================================== */
+/* one frame through the GPU (reference compress_engine, cmp.c:213-338) */
+/* ================================================================== */
+enum sample_kind { KIND_I16 = 0, KIND_I16_IN_I32 = 1, KIND_U16 = 2 };
+
+struct frame_io {
+	const void *src;   /* host or device, see `device` */
+	uint32_t n;        /* samples */
+	uint32_t bytes;    /* 2 or 4 per sample */
+	enum sample_kind kind;
+	int device;        /* src/dst/work_buf are device pointers (cmp_gpu.h path) */
+	struct airs_dev_engine *dev;
+	/* device-mode extras */
+	uint32_t *d_status;
+};
+
+/* the pass a frame will use, resolved from the context (cmp.c:228-248) */
+struct pass {
+	uint32_t pre, enc, par, outlier_param, outlier;
+	uint32_t model_mode;
+	uint32_t seq;
+	uint32_t hdr_bytes;
+};
+
+enum { SLOT_SRC = 0, SLOT_DST, SLOT_MODEL, SLOT_STATUS, SLOT_CK, SLOT_IDS, SLOT_G, SLOT_AUX };
+
+static struct airs_dev_engine *g_host_dev;
+
+static struct airs_dev_engine *host_dev(void)
+{
+	if (!g_host_dev) {
+		g_host_dev = airs_dev_engine_create(NULL);
+		if (!g_host_dev)
+			fprintf(stderr, "airscmp: no usable GPU (%s); libairscmp has no CPU encode path\n",
+				airs_dev_last_error());
+	}
+	return g_host_dev;
+}
+
+/* checks and state updates of compress_engine up to the encode loop;
+ * returns 0 (pass filled in) or the error the reference would return */
+static uint32_t engine_prologue(struct cmp_context *ctx, void *dst, uint32_t cap, uint32_t n, struct pass *p)
+{
+	const uint32_t packed = 2u * n;
+	uint32_t e;
+
+	memset(p, 0, sizeof(*p));
+	if (ctx->sequence_number == 0 || ctx->sequence_number > ctx->params.secondary_iterations) {
+		e = cmp_reset(ctx);
+		if (is_err(e))
+			return e;
+		p->pre = ctx->params.primary_preprocessing;
+		p->enc = ctx->params.primary_encoder_type;
+		p->par = ctx->params.primary_encoder_param;
+		p->outlier_param = ctx->params.primary_encoder_outlier;
+		ctx->model_size = packed;
+	} else {
+		p->pre = ctx->params.secondary_preprocessing;
+		p->enc = ctx->params.secondary_encoder_type;
+		p->par = ctx->params.secondary_encoder_param;
+		p->outlier_param = ctx->params.secondary_encoder_outlier;
+		if (model_needed(&ctx->params) && packed != ctx->model_size)
+			return ERRV(SRC_SIZE_MISMATCH);
+	}
+	if (model_needed(&ctx->params) && ctx->work_buf_size < packed)
+		return ERRV(WORK_BUF_TOO_SMALL);
+	if (!dst)
+		return ERRV(DST_NULL);
+	if ((uintptr_t)dst & 7u)
+		return ERRV(DST_UNALIGNED);
+	e = coder_resolve(p->enc, p->par, p->outlier_param, &p->outlier);
+	if (is_err(e))
+		return e;
+	p->hdr_bytes = (p->pre == CMP_PREPROCESS_NONE && p->enc == CMP_ENCODER_UNCOMPRESSED) ? CMP_HDR_SIZE
+											   : HDR_MAX_SIZE;
+	/* header serialisation (header.c:24-67): original size, then the flush */
+	if (packed > CMP_HDR_MAX_ORIGINAL_SIZE)
+		return ERRV(HDR_ORIGINAL_TOO_LARGE);
+	if (cap < p->hdr_bytes)
+		return ERRV(DST_TOO_SMALL);
+	/* preprocessing init (preprocess.c:321-393) */
+	if (p->pre == CMP_PREPROCESS_IWT || p->pre == CMP_PREPROCESS_MODEL) {
+		if (!ctx->work_buf)
+			return ERRV(WORK_BUF_NULL);
+		if (ctx->work_buf_size < ((packed + 1u) & ~1u))
+			return ERRV(WORK_BUF_TOO_SMALL);
+		if ((uintptr_t)ctx->work_buf & 1u)
+			return ERRV(WORK_BUF_UNALIGNED);
+	} else if (p->pre != CMP_PREPROCESS_NONE && p->pre != CMP_PREPROCESS_DIFF) {
+		return ERRV(PARAMS_INVALID);
+	}
+	if (p->pre == CMP_PREPROCESS_IWT) {
+		fprintf(stderr, "airscmp: IWT preprocessing is not implemented on the GPU yet\n");
+		return ERRV(GENERIC);
+	}
+	p->model_mode = model_needed(&ctx->params) ?
+				(ctx->sequence_number == 0 ? AIRS_MODEL_STORE : AIRS_MODEL_UPDATE) :
+				AIRS_MODEL_NONE;
+	p->seq = ctx->sequence_number;
+	return 0;
+}
+
+/* bit position whose flush fails for capacity cap: samples reaching it keep
+ * their old model (cmp.c:300-302 breaks the loop before the model update) */
+static uint64_t model_fail_bit(uint32_t cap, uint32_t n)
+{
+	uint32_t bound = cmp_compress_bound(2u * n);
+
+	if (!is_err(bound) && cap >= bound)
+		return UINT64_MAX;
+	return 64ull * (cap / 8u) + 63ull;
+}
+
+/* largest possible frame for n samples: header + 48 bits/sample + checksum */
+static uint64_t frame_worst(uint32_t n)
+{
+	return HDR_MAX_SIZE + CMP_CHECKSUM_SIZE + payload_bound(2u * n) + 8u;
+}
+
+/* Host-pointer frame: stage through device scratch, run, copy back. */
+static uint32_t host_engine(struct cmp_context *ctx, void *dst, uint32_t cap, const struct frame_io *io)
+{
+	struct pass p;
+	struct airs_launch L;
+	struct airs_dev_engine *dev;
+	uint32_t e, st[2] = { 0, 0 };
+	uint64_t worst = frame_worst(io->n);
+	uint32_t kcap = (uint64_t)cap < worst ? cap : (uint32_t)worst;
+	const uint32_t packed = 2u * io->n;
+	void *d_src, *d_dst, *d_model = NULL, *d_status, *d_ck = NULL;
+
+	e = engine_prologue(ctx, dst, cap, io->n, &p);
+	if (is_err(e))
+		return e;
+	dev = host_dev();
+	if (!dev)
+		return ERRV(GENERIC);
+
+	d_src = airs_dev_scratch(dev, SLOT_SRC, (size_t)io->n * io->bytes);
+	d_dst = airs_dev_scratch(dev, SLOT_DST, (size_t)worst);
+	d_status = airs_dev_scratch(dev, SLOT_STATUS, 64);
+	if (!d_src || !d_dst || !d_status)
+		return ERRV(GENERIC);
+	if (is_err(airs_dev_h2d(dev, d_src, io->src, (size_t)io->n * io->bytes)))
+		return ERRV(GENERIC);
+	if (p.model_mode != AIRS_MODEL_NONE) {
+		d_model = airs_dev_scratch(dev, SLOT_MODEL, (size_t)packed + 16u);
+		if (!d_model || is_err(airs_dev_h2d(dev, d_model, ctx->work_buf, packed)))
+			return ERRV(GENERIC);
+	}
+	if (ctx->params.checksum_enabled) {
+		d_ck = airs_dev_scratch(dev, SLOT_CK, 64);
+		if (!d_ck || is_err(airs_dev_checksum(dev, d_src, 0, io->bytes, io->n, 1, NULL, d_ck)))
+			return ERRV(GENERIC);
+	}
+
+	memset(&L, 0, sizeof(L));
+	L.src = d_src;
+	L.sample_bytes = io->bytes;
+	L.is_unsigned = io->kind == KIND_U16;
+	L.n = io->n;
+	L.num_frames = 1;
+	L.frame_mul = 1;
+	L.dst = d_dst;
+	L.cap = kcap;
+	L.preprocessing = p.pre;
+	L.encoder_type = p.enc;
+	L.encoder_param = p.par;
+	L.outlier_param = p.outlier_param;
+	L.model = d_model;
+	L.model_div = 1;
+	L.model_mode = p.model_mode;
+	L.model_rate = ctx->params.model_rate;
+	L.fail_bit = model_fail_bit(cap, io->n);
+	L.id_base = ctx->identifier;
+	L.seq = p.seq;
+	L.checksum_enabled = ctx->params.checksum_enabled ? 1u : 0u;
+	L.checksums = d_ck;
+	L.status = d_status;
+	L.needed = (uint32_t *)d_status + 1;
+	e = airs_dev_encode(dev, &L);
+	if (is_err(e))
+		return e;
+	if (is_err(airs_dev_d2h(dev, st, d_status, sizeof(st))))
+		return ERRV(GENERIC);
+	if (p.model_mode != AIRS_MODEL_NONE && is_err(airs_dev_d2h(dev, ctx->work_buf, d_model, packed)))
+		return ERRV(GENERIC);
+	if (is_err(airs_dev_sync(dev)))
+		return ERRV(GENERIC);
+	if (is_err(st[0]))
+		return st[0];
+	if (is_err(airs_dev_d2h(dev, dst, d_dst, st[0])) || is_err(airs_dev_sync(dev)))
+		return ERRV(GENERIC);
+	ctx->sequence_number++;
+	return st[0];
+}
+
+/* uncompressed fallback (reference cmp_compress_generic, cmp.c:342-393) */
+static uint32_t host_generic(struct cmp_context *ctx, void *dst, uint32_t cap, const struct frame_io *io)
+{
+	uint32_t raw = CMP_HDR_SIZE + 2u * io->n, r;
+	enum cmp_preprocessing save_pre;
+	enum cmp_encoder_type save_enc;
+
+	if (!ctx)
+		return ERRV(GENERIC);
+	if (ctx->magic != CTX_MAGIC)
+		return ERRV(CONTEXT_INVALID);
+	if (is_err(cap))
+		return ERRV(GENERIC);
+	if (ctx->params.checksum_enabled)
+		raw += CMP_CHECKSUM_SIZE;
+	if (!ctx->params.uncompressed_fallback_enabled || cap < raw)
+		return host_engine(ctx, dst, cap, io);
+	r = host_engine(ctx, dst, raw, io);
+	if (cmp_get_error_code(r) != CMP_ERR_DST_TOO_SMALL)
+		return r;
+	r = cmp_reset(ctx);
+	if (is_err(r))
+		return r;
+	save_pre = ctx->params.primary_preprocessing;
+	save_enc = ctx->params.primary_encoder_type;
+	ctx->params.primary_preprocessing = CMP_PREPROCESS_NONE;
+	ctx->params.primary_encoder_type = CMP_ENCODER_UNCOMPRESSED;
+	r = host_engine(ctx, dst, raw, io);
+	ctx->params.primary_preprocessing = save_pre;
+	ctx->params.primary_encoder_type = save_enc;
+	return r;
+}
+
+static uint32_t host_compress(struct cmp_context *ctx, void *dst, uint32_t cap, const void *src,
+			      uint32_t size, enum sample_kind kind)
+{
+	struct frame_io io;
+	uint32_t stride = kind == KIND_I16_IN_I32 ? 4u : 2u;
+
+	/* reference sample_reader.h:19-51 */
+	if (!src)
+		return ERRV(SRC_NULL);
+	if (size == 0 || size % stride)
+		return ERRV(SRC_SIZE_WRONG);
+	memset(&io, 0, sizeof(io));
+	io.src = src;
+	io.n = size / stride;
+	io.bytes = stride;
+	io.kind = kind;
+	return host_generic(ctx, dst, cap, &io);
+}
+
+uint32_t cmp_compress_u16(struct cmp_context *ctx, void *dst, uint32_t dst_capacity, const uint16_t *src,
+			  uint32_t src_size)
+{
+	return host_compress(ctx, dst, dst_capacity, src, src_size, KIND_U16);
+}
+
+uint32_t cmp_compress_i16(struct cmp_context *ctx, void *dst, uint32_t dst_capacity, const int16_t *src,
+			  uint32_t src_size)
+{
+	return host_compress(ctx, dst, dst_capacity, src, src_size, KIND_I16);
+}
+
+uint32_t cmp_compress_i16_in_i32(struct cmp_context *ctx, void *dst, uint32_t dst_capacity,
+				 const int32_t *src, uint32_t src_size)
+{
+	return host_compress(ctx, dst, dst_capacity, src, src_size, KIND_I16_IN_I32);
+}
+
+/* ================================================================== */
+/* device batch API (cmp_gpu.h)                                       */
+/* ================================================================== */
+struct cmp_gpu_engine {
+	struct airs_dev_engine *dev;
+};
+
+int cmp_gpu_available(void)
+{
+	return airs_dev_available();
+}
+
+uint32_t cmp_gpu_engine_create(struct cmp_gpu_engine **engine, void *hip_stream)
+{
+	struct cmp_gpu_engine *g;
+
+	if (!engine)
+		return ERRV(GENERIC);
+	*engine = NULL;
+	g = calloc(1, sizeof(*g));
+	if (!g)
+		return ERRV(GENERIC);
+	g->dev = airs_dev_engine_create(hip_stream);
+	if (!g->dev) {
+		fprintf(stderr, "airscmp: cannot create GPU engine (%s)\n", airs_dev_last_error());
+		free(g);
+		return ERRV(GENERIC);
+	}
+	*engine = g;
+	return 0;
+}
+
+void cmp_gpu_engine_destroy(struct cmp_gpu_engine *engine)
+{
+	if (!engine)
+		return;
+	airs_dev_engine_destroy(engine->dev);
+	free(engine);
+}
+
+uint32_t cmp_gpu_synchronize(struct cmp_gpu_engine *engine)
+{
+	if (!engine)
+		return ERRV(GENERIC);
+	return airs_dev_sync(engine->dev);
+}
+
+uint32_t cmp_gpu_synthesize(struct cmp_gpu_engine *engine, void *dst, uint32_t sample_bytes, uint64_t seed,
+			    uint32_t frame0, uint32_t samples_per_frame, uint32_t num_frames, uint64_t stride,
+			    uint32_t noise_w)
+{
+	if (!engine || !dst || (sample_bytes != 2 && sample_bytes != 4))
+		return ERRV(GENERIC);
+	return airs_dev_synth(engine->dev, dst, sample_bytes, seed, frame0, samples_per_frame, num_frames,
+			      stride, noise_w);
+}
+
+/* per-frame plan of a batch, computed by replaying the context state machine */
+struct frame_plan {
+	struct pass p;
+	uint64_t id;
+	uint32_t err; /* host-detected error for this frame, or 0 */
+};
+
+static int same_pass(const struct pass *a, const struct pass *b)
+{
+	return a->pre == b->pre && a->enc == b->enc && a->par == b->par &&
+	       a->outlier_param == b->outlier_param && a->model_mode == b->model_mode && a->seq == b->seq;
+}
+
+/* is v[j] = v[0] + j*step for all j?  (step returned) */
+static int affine_u64(const uint64_t *v, uint32_t cnt, uint64_t *step)
+{
+	uint32_t j;
+
+	*step = cnt > 1 ? v[1] - v[0] : 0;
+	for (j = 2; j < cnt; j++)
+		if (v[j] - v[j - 1] != *step)
+			return 0;
+	return 1;
+}
+
+/* launch the frames j -> batch frame (add + j*mul), j < cnt, all with pass P */
+static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t fpc,
+			     const struct cmp_gpu_batch *b, const struct frame_plan *plan, uint32_t add,
+			     uint32_t mul, uint32_t cnt, uint64_t *ids_scratch, uint64_t *ptr_scratch)
+{
+	struct airs_dev_engine *dev = eng->dev;
+	const struct pass *P = &plan[add].p;
+	const struct cmp_params *prm = &ctx[add / fpc].params;
+	const uint32_t bytes = b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
+	const uint32_t n = b->src_size / bytes;
+	const uint32_t nframes_total = (add + (cnt - 1) * mul) + 1;
+	struct airs_launch L;
+	uint64_t step, worst = frame_worst(n);
+	uint32_t j, e, *d_g = NULL, *d_ck = NULL;
+
+	memset(&L, 0, sizeof(L));
+	for (j = 0; j < cnt; j++)
+		ids_scratch[j] = plan[add + j * mul].id;
+	if (affine_u64(ids_scratch, cnt, &step)) {
+		L.id_base = ids_scratch[0];
+		L.id_step = step;
+	} else {
+		uint64_t *d_ids = airs_dev_scratch(dev, SLOT_IDS, (size_t)cnt * 8u);
+
+		if (!d_ids || is_err(airs_dev_h2d(dev, d_ids, ids_scratch, (size_t)cnt * 8u)) ||
+		    is_err(airs_dev_sync(dev)))
+			return ERRV(GENERIC);
+		L.ids = d_ids;
+	}
+	if (P->model_mode != AIRS_MODEL_NONE) {
+		for (j = 0; j < cnt; j++)
+			ptr_scratch[j] = (uint64_t)(uintptr_t)ctx[(add + j * mul) / fpc].work_buf;
+		/* model of frame f = base + (f / fpc) * stride when the work buffers are strided */
+		{
+			uint64_t base = (uint64_t)(uintptr_t)ctx[0].work_buf, mstep = 0;
+			uint32_t c, ok = 1, nctx = (nframes_total + fpc - 1) / fpc;
+
+			if (nctx > 1)
+				mstep = (uint64_t)(uintptr_t)ctx[1].work_buf - base;
+			for (c = 0; c < nctx && ok; c++)
+				ok = (uint64_t)(uintptr_t)ctx[c].work_buf == base + c * mstep;
+			if (ok) {
+				L.model = (void *)(uintptr_t)base;
+				L.model_stride = mstep;
+				L.model_div = fpc;
+			} else {
+				uint64_t *d_ptr = airs_dev_scratch(dev, SLOT_AUX, (size_t)cnt * 8u);
+
+				if (!d_ptr || is_err(airs_dev_h2d(dev, d_ptr, ptr_scratch, (size_t)cnt * 8u)) ||
+				    is_err(airs_dev_sync(dev)))
+					return ERRV(GENERIC);
+				L.model_ptrs = d_ptr;
+			}
+		}
+	}
+	if (prm->checksum_enabled) {
+		d_ck = airs_dev_scratch(dev, SLOT_CK, (size_t)nframes_total * 4u);
+		if (!d_ck)
+			return ERRV(GENERIC);
+		/* the checksum kernel takes a frame list: reuse the affine map via a
+		 * contiguous range when mul == 1, else hash every frame up to the last */
+		e = airs_dev_checksum(dev, b->src, b->src_stride, bytes, n, nframes_total, NULL, d_ck);
+		if (is_err(e))
+			return e;
+	}
+	if ((b->flags & CMP_GPU_AUTO_RICE) && P->enc == CMP_ENCODER_GOLOMB_ZERO) {
+		d_g = airs_dev_scratch(dev, SLOT_G, (size_t)nframes_total * 4u);
+		if (!d_g)
+			return ERRV(GENERIC);
+		e = airs_dev_select_rice(dev, b->src, b->src_stride, bytes, n, nframes_total, P->pre, d_g);
+		if (is_err(e))
+			return e;
+	}
+	L.src = b->src;
+	L.src_stride = b->src_stride;
+	L.sample_bytes = bytes;
+	L.is_unsigned = b->type == CMP_GPU_U16;
+	L.n = n;
+	L.num_frames = cnt;
+	L.frame_add = add;
+	L.frame_mul = mul;
+	L.dst = b->dst;
+	L.dst_stride = b->dst_stride;
+	L.cap = (uint64_t)b->dst_capacity < worst ? b->dst_capacity : (uint32_t)worst;
+	L.preprocessing = P->pre;
+	L.encoder_type = P->enc;
+	L.encoder_param = P->par;
+	L.outlier_param = P->outlier_param;
+	L.frame_g = d_g;
+	L.model_mode = P->model_mode;
+	L.model_rate = prm->model_rate;
+	L.fail_bit = model_fail_bit(b->dst_capacity, n);
+	L.seq = P->seq;
+	L.checksum_enabled = prm->checksum_enabled ? 1u : 0u;
+	L.checksums = d_ck;
+	L.status = b->sizes;
+	return airs_dev_encode(dev, &L);
+}
+
+uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx,
+			  uint32_t fpc, const struct cmp_gpu_batch *b)
+{
+	const uint32_t bytes = b && b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
+	uint32_t n, c, a, total, e = 0, any_model = 0;
+	struct frame_plan *plan;
+	uint64_t *ids, *ptrs;
+
+	if (!eng || !ctx || !b || !num_ctx || !fpc)
+		return ERRV(GENERIC);
+	if (b->type > CMP_GPU_I16_IN_I32)
+		return ERRV(PARAMS_INVALID);
+	if (!b->src)
+		return ERRV(SRC_NULL);
+	if (b->src_size == 0 || b->src_size % bytes)
+		return ERRV(SRC_SIZE_WRONG);
+	if (((uintptr_t)b->src % bytes) || (b->src_stride % bytes)) {
+		fprintf(stderr, "airscmp: cmp_gpu_compress: src must be %u-byte aligned\n", bytes);
+		return ERRV(GENERIC);
+	}
+	if (!b->sizes) {
+		fprintf(stderr, "airscmp: cmp_gpu_compress: sizes array is NULL\n");
+		return ERRV(GENERIC);
+	}
+	if (!b->dst)
+		return ERRV(DST_NULL);
+	if (((uintptr_t)b->dst & 7u) || (b->dst_stride & 7u))
+		return ERRV(DST_UNALIGNED);
+	if (is_err(b->dst_capacity))
+		return ERRV(GENERIC);
+	if ((uint64_t)num_ctx * fpc > 0xFFFFFFFull)
+		return ERRV(PARAMS_INVALID);
+	n = b->src_size / bytes;
+	total = num_ctx * fpc;
+	for (c = 0; c < num_ctx; c++) {
+		if (ctx[c].magic != CTX_MAGIC)
+			return ERRV(CONTEXT_INVALID);
+		if (ctx[c].params.uncompressed_fallback_enabled &&
+		    b->dst_capacity >= CMP_HDR_SIZE + 2u * n + (ctx[c].params.checksum_enabled ? 4u : 0u)) {
+			/* fallback needs the exact frame-by-frame protocol */
+			fprintf(stderr, "airscmp: cmp_gpu_compress: uncompressed_fallback_enabled is not "
+					"supported by the batch API yet; use cmp_compress_*\n");
+			return ERRV(PARAMS_INVALID);
+		}
+		if (model_needed(&ctx[c].params)) {
+			any_model = 1;
+			if ((uintptr_t)ctx[c].work_buf & 1u)
+				return ERRV(WORK_BUF_UNALIGNED);
+		}
+	}
+
+	plan = calloc(total, sizeof(*plan));
+	ids = calloc(total, sizeof(*ids));
+	ptrs = calloc(total, sizeof(*ptrs));
+	if (!plan || !ids || !ptrs) {
+		free(plan);
+		free(ids);
+		free(ptrs);
+		return ERRV(GENERIC);
+	}
+	/* replay the context state machine in call order (c-major), assuming
+	 * every frame succeeds; this draws the identifiers in reference order */
+	for (c = 0; c < num_ctx && !e; c++) {
+		for (a = 0; a < fpc && !e; a++) {
+			struct frame_plan *fp = &plan[c * fpc + a];
+			void *dst = (uint8_t *)b->dst + (uint64_t)(c * fpc + a) * b->dst_stride;
+
+			e = engine_prologue(&ctx[c], dst, b->dst_capacity, n, &fp->p);
+			if (is_err(e))
+				break;
+			fp->id = ctx[c].identifier;
+			ctx[c].sequence_number++;
+		}
+	}
+	if (is_err(e))
+		goto out;
+
+	/* launch: frames with equal passes share one launch; MODEL contexts
+	 * step through acquisitions in order (the model carries state) */
+	if (!any_model && (num_ctx == 1 || fpc == 1)) {
+		/* contiguous runs of frames with the same pass, one launch each */
+		uint32_t f = 0;
+
+		while (f < total && !is_err(e)) {
+			uint32_t g = f + 1;
+
+			while (g < total && same_pass(&plan[g].p, &plan[f].p))
+				g++;
+			e = batch_launch(eng, ctx, fpc, b, plan, f, 1, g - f, ids, ptrs);
+			f = g;
+		}
+	} else {
+		uint32_t f, uniform = 1;
+
+		for (f = 1; f < total && uniform; f++)
+			uniform = same_pass(&plan[f].p, &plan[0].p);
+		if (uniform && !any_model) {
+			e = batch_launch(eng, ctx, fpc, b, plan, 0, 1, total, ids, ptrs);
+		} else {
+			/* one launch per acquisition step across the contexts; MODEL
+			 * contexts carry state from one step to the next */
+			for (a = 0; a < fpc && !is_err(e); a++) {
+				for (c = 1; c < num_ctx; c++)
+					if (!same_pass(&plan[c * fpc + a].p, &plan[a].p))
+						break;
+				if (c < num_ctx) {
+					fprintf(stderr, "airscmp: cmp_gpu_compress: contexts in different "
+							"states cannot share a batch\n");
+					e = ERRV(PARAMS_INVALID);
+					break;
+				}
+				e = batch_launch(eng, ctx, fpc, b, plan, a, fpc, num_ctx, ids, ptrs);
+			}
+		}
+	}
+out:
+	free(plan);
+	free(ids);
+	free(ptrs);
+	return is_err(e) ? e : 0;
+}

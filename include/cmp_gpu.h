@@ -1,0 +1,91 @@
+/*
+ * cmp_gpu.h -- device-pointer batch API of the MI355X build (libairscmp.so).
+ *
+ * No reference counterpart: the reference (lib/cmp.h) compresses one frame
+ * from host memory per call.  This API runs the same frame format and the
+ * same cmp_context state machine (lib/compress/cmp.c:213-393) over many
+ * frames whose samples already live in GPU memory, with one launch per group
+ * of frames that share pass parameters.  Frames produced here are
+ * byte-identical to what cmp_compress_u16/i16/i16_in_i32 produce for the
+ * same inputs, contexts and identifiers.
+ *
+ * Contexts come from cmp_initialise() exactly as for the host API; when a
+ * context needs a work buffer (MODEL preprocessing) its work_buf must be a
+ * DEVICE pointer (2-byte aligned; 16 is fastest) holding that context's model.
+ *
+ * Ordering / identifiers: a call is equivalent to
+ *
+ *     for c in [0, num_ctx): for a in [0, frames_per_ctx):
+ *         sizes[c*fpc + a] = cmp_compress_<type>(&ctx[c], dst(c*fpc+a), dst_capacity,
+ *                                                src(c*fpc+a), src_size)
+ *
+ * including the timestamp-callback sequence that feeds header identifiers.
+ */
+#ifndef CMP_GPU_H
+#define CMP_GPU_H
+
+#include <stdint.h>
+
+#include "cmp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* sample layout of the frames in a batch (the three cmp_compress_* entry points) */
+enum cmp_gpu_sample_type {
+	CMP_GPU_U16 = 0,       /* cmp_compress_u16 */
+	CMP_GPU_I16 = 1,       /* cmp_compress_i16 */
+	CMP_GPU_I16_IN_I32 = 2 /* cmp_compress_i16_in_i32 */
+};
+
+/* flags */
+#define CMP_GPU_AUTO_RICE 0x1u /* GOLOMB_ZERO passes: choose g = 2^k per frame (k in [0,15],
+				* fewest payload bits, ties to smaller k) instead of the
+				* configured encoder parameter; build-defined extension */
+
+struct cmp_gpu_batch {
+	enum cmp_gpu_sample_type type;
+	const void *src;        /* device; frame i at src + i*src_stride (16-byte aligned frames load fastest) */
+	uint64_t src_stride;    /* bytes, multiple of the sample size */
+	uint32_t src_size;      /* bytes per frame, as cmp_compress_*'s src_size */
+	void *dst;              /* device; frame i at dst + i*dst_stride, 8-byte aligned */
+	uint64_t dst_stride;    /* bytes, multiple of 8 */
+	uint32_t dst_capacity;  /* bytes available per frame */
+	uint32_t *sizes;        /* device [num frames]: frame size or error value */
+	uint32_t flags;
+};
+
+struct cmp_gpu_engine;
+
+/* Create an engine bound to the current HIP device and the given hipStream_t
+ * (NULL = default stream).  Returns an error value or CMP_ERR_NO_ERROR. */
+uint32_t cmp_gpu_engine_create(struct cmp_gpu_engine **engine, void *hip_stream);
+void cmp_gpu_engine_destroy(struct cmp_gpu_engine *engine);
+
+/* Compress num_ctx * frames_per_ctx frames (see the ordering note above).
+ * Returns CMP_ERR_NO_ERROR or a call-level error (validation, as the host API
+ * would report it for the first frame).  Per-frame results land in
+ * batch->sizes.  The call is asynchronous on the engine's stream unless a
+ * context has uncompressed_fallback_enabled, in which case it synchronises
+ * once per acquisition step to resolve fallbacks exactly. */
+uint32_t cmp_gpu_compress(struct cmp_gpu_engine *engine, struct cmp_context *ctx, uint32_t num_ctx,
+			  uint32_t frames_per_ctx, const struct cmp_gpu_batch *batch);
+
+/* wait for all work queued on the engine */
+uint32_t cmp_gpu_synchronize(struct cmp_gpu_engine *engine);
+
+/* Fill num_frames device frames with the counter-hash synthetic signal used by
+ * the benchmark (sample_bytes 2: u16; 4: i16-in-i32 with junk upper halves). */
+uint32_t cmp_gpu_synthesize(struct cmp_gpu_engine *engine, void *dst, uint32_t sample_bytes,
+			    uint64_t seed, uint32_t frame0, uint32_t samples_per_frame,
+			    uint32_t num_frames, uint64_t stride, uint32_t noise_w);
+
+/* non-zero when a GPU is present and the HIP runtime initialised */
+int cmp_gpu_available(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CMP_GPU_H */
