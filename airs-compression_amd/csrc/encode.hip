@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "airs_dev.h"
@@ -79,6 +80,7 @@ struct KArgs {
 	uint32_t model_mode, model_rate, is_unsigned, checksum;
 	uint32_t seq, pre_hdr, enc_hdr, model_rate_hdr;
 	uint32_t ticket_base, epoch;
+	uint32_t dbg; // ablation switches (AIRS_DBG env, benchmarking only; 0 in production)
 };
 
 // ---------------------------------------------------------------------
@@ -130,35 +132,68 @@ __device__ __forceinline__ void golomb(uint32_t v, const Coder &c, uint32_t &cw,
 	}
 }
 
-// One residual (16-bit pattern) -> up to two (codeword, length) pieces
-// (reference encoder.c:327-378; ZigZag :274-286).
+__device__ __forceinline__ uint32_t zigzag16(uint32_t u) // u: 16-bit residual pattern
+{
+	return ((u << 1) ^ (0u - ((u >> 15) & 1u))) & 0xFFFFu; // reference encoder.c:274-286
+}
+
+// v_bfm_b32: ((1 << w) - 1) << o, using the low 5 bits of w and o (no UB for
+// the discarded escape lanes whose w is out of range)
+__device__ __forceinline__ uint32_t bfm32(uint32_t w, uint32_t o)
+{
+	uint32_t r;
+	asm("v_bfm_b32 %0, %1, %2" : "=v"(r) : "v"(w), "v"(o));
+	return r;
+}
+
+// Mapped value (ZigZag, or the raw residual for UNCOMPRESSED) -> up to two
+// (codeword, length) pieces (reference encoder.c:327-378).
 template <int ENC, bool RICE>
-__device__ __forceinline__ void code_sample(uint32_t u, const Coder &c, uint32_t &cw1, uint32_t &l1,
+__device__ __forceinline__ void code_from_m(uint32_t m, const Coder &c, uint32_t &cw1, uint32_t &l1,
 					    uint32_t &cw2, uint32_t &l2)
 {
+	cw2 = 0u;
+	l2 = 0u;
 	if (ENC == ENC_RAW) {
-		cw1 = u & 0xFFFFu;
+		cw1 = m;
 		l1 = 16u;
-		cw2 = 0u;
-		l2 = 0u;
 		return;
 	}
-	const uint32_t m = ((u << 1) ^ (0u - ((u >> 15) & 1u))) & 0xFFFFu;
-	const bool esc = m >= c.outlier;
 	if (ENC == ENC_ZERO) {
-		uint32_t gcw, glen;
-		golomb<RICE>(m + 1u, c, gcw, glen);
-		cw1 = esc ? m : gcw;                 // zero codeword + 16 raw bits in one piece
-		l1 = esc ? c.k + 17u : glen;
-		cw2 = 0u;
-		l2 = 0u;
-	} else {
-		const uint32_t d = m - c.outlier;
-		const uint32_t lvl = d < 4u ? 0u : (31u - (uint32_t)__clz((int)d)) >> 1;
-		golomb<RICE>(esc ? c.outlier + lvl : m, c, cw1, l1);
-		cw2 = esc ? d : 0u;
-		l2 = esc ? 2u * (lvl + 1u) : 0u;
+		if (RICE) {
+			// g = 2^k: v = m + 1, q = v >> k; the zero-escape length k+17 is
+			// exactly the q = 16 case of k + 1 + q, so the length needs no select
+			const uint32_t v = m + 1u, q = v >> c.k;
+			l1 = c.k + 1u + min(q, 16u);
+			cw1 = q > 16u ? m : (bfm32(q, c.k + 1u) | (v & (c.g - 1u)));
+		} else {
+			uint32_t gcw, glen;
+			golomb<false>(m + 1u, c, gcw, glen);
+			const bool esc = m >= c.outlier;
+			cw1 = esc ? m : gcw; // zero codeword + 16 raw bits in one piece
+			l1 = esc ? c.k + 17u : glen;
+		}
+		return;
 	}
+	const bool esc = m >= c.outlier;
+	const uint32_t d = m - c.outlier;
+	const uint32_t lvl = d < 4u ? 0u : (31u - (uint32_t)__clz((int)d)) >> 1;
+	golomb<RICE>(esc ? c.outlier + lvl : m, c, cw1, l1);
+	cw2 = esc ? d : 0u;
+	l2 = esc ? 2u * (lvl + 1u) : 0u;
+}
+
+// code length only (the lengths pass)
+template <int ENC, bool RICE>
+__device__ __forceinline__ uint32_t len_from_m(uint32_t m, const Coder &c)
+{
+	if (ENC == ENC_RAW)
+		return 16u;
+	if (ENC == ENC_ZERO && RICE)
+		return c.k + 1u + min((m + 1u) >> c.k, 16u);
+	uint32_t cw1, l1, cw2, l2;
+	code_from_m<ENC, RICE>(m, c, cw1, l1, cw2, l2);
+	return l1 + l2;
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t v)
@@ -223,281 +258,547 @@ __device__ __forceinline__ void load16_model(const uint8_t *m, uint32_t first, u
 	load16<2>(m, first, n, x);
 }
 
-// Header bytes 0..21 of a frame (reference header.c:24-67), big-endian.
-__device__ __forceinline__ void header_bytes(uint8_t (&h)[24], uint32_t size, uint32_t orig, uint64_t id,
-					     uint32_t seq, uint32_t pre, uint32_t ck, uint32_t enc,
-					     uint32_t rate, uint32_t par, uint32_t outl)
+// Header dwords 0..4 of a frame (reference header.c:24-67), big-endian
+// values; bytes 20-21 (outlier low half) travel with the first payload dword.
+__device__ __forceinline__ void header_words(uint32_t (&h)[5], uint32_t size, uint32_t orig, uint64_t id,
+					     uint32_t seq, uint32_t pre, uint32_t ck, uint32_t enc, uint32_t rate,
+					     uint32_t par, uint32_t outl)
 {
-	h[0] = 0x80u | (600u >> 8);
-	h[1] = 600u & 0xFFu;
-	h[2] = (uint8_t)(size >> 16);
-	h[3] = (uint8_t)(size >> 8);
-	h[4] = (uint8_t)size;
-	h[5] = (uint8_t)(orig >> 16);
-	h[6] = (uint8_t)(orig >> 8);
-	h[7] = (uint8_t)orig;
-	for (int b = 0; b < 6; b++)
-		h[8 + b] = (uint8_t)(id >> (40 - 8 * b));
-	h[14] = (uint8_t)seq;
-	h[15] = (uint8_t)((pre << 4) | (ck << 3) | enc);
-	h[16] = (uint8_t)rate;
-	h[17] = (uint8_t)(par >> 8);
-	h[18] = (uint8_t)par;
-	h[19] = (uint8_t)(outl >> 16);
-	h[20] = (uint8_t)(outl >> 8);
-	h[21] = (uint8_t)outl;
-	h[22] = 0;
-	h[23] = 0;
+	h[0] = (0x8000u | 600u) << 16 | (size >> 8);
+	h[1] = (size & 0xFFu) << 24 | (orig & 0xFFFFFFu);
+	h[2] = (uint32_t)(id >> 16);
+	h[3] = (uint32_t)(id & 0xFFFFu) << 16 | (seq & 0xFFu) << 8 | (pre << 4 | ck << 3 | enc);
+	h[4] = (rate & 0xFFu) << 24 | (par & 0xFFFFu) << 8 | ((outl >> 16) & 0xFFu);
+}
+
+// DPP inclusive prefix sum over the 64 lanes of a wave (GFX9 row_shr +
+// row_bcast sequence; no LDS traffic).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false); // row_shr:1
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false); // row_shr:2
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false); // row_shr:4
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false); // row_shr:8
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false); // row_bcast:15
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false); // row_bcast:31
+	return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+	return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
 }
 
 // ---------------------------------------------------------------------
 // the encode kernel
+//   W      bytes per input sample (2: u16/i16, 4: i16 in i32)
+//   PRE    NONE / DIFF / MODEL
+//   ENC    UNCOMPRESSED / GOLOMB_ZERO / GOLOMB_MULTI
+//   RICE   Golomb parameter is a power of two (shift instead of divide)
+//   MODEL  0: no model, 1: store samples (primary pass), 2: update (secondary)
+//
+// One workgroup encodes one segment of SEG_CHUNKS(W, MODEL) chunks of 4096
+// samples; lane t owns samples [16t, 16t+16) of every chunk.  All chunk loads
+// are issued up front (32 KiB per workgroup for u16) so HBM sees many bytes in
+// flight per CU.  Phase 1 computes only code lengths, so the segment's bit
+// total and its last 32 bits are published early; phase 2 rebuilds the
+// codewords chunk by chunk into a double-buffered LDS image and stores them
+// once the look-back has produced the segment's frame bit offset.
 // ---------------------------------------------------------------------
-template <int W, int PRE, int ENC, bool RICE>
+__host__ __device__ constexpr uint32_t seg_chunks(int W, int MODEL)
+{
+	return (W == 4 || MODEL) ? 2u : 4u;
+}
+
+template <int W, int PRE, int ENC, bool RICE, int MODEL>
 __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 {
+	constexpr uint32_t CH = seg_chunks(W, MODEL);
+	constexpr uint32_t SEGN = CH * AIRS_SEG;
 	constexpr uint32_t MAXBITS = ENC == ENC_RAW ? 16u : (ENC == ENC_ZERO ? 32u : 48u);
-	constexpr uint32_t LWORDS = AIRS_SEG * MAXBITS / 32u + 2u;
-	__shared__ uint32_t L[LWORDS];
-	__shared__ uint32_t s_misc[16];
+	constexpr uint32_t LWORDS = AIRS_SEG * MAXBITS / 32u + 4u; // one chunk image
+	constexpr uint32_t NPIECE = ENC == ENC_MULTI ? 2 : 1;
+	constexpr uint32_t RW = W == 2 ? 2u : 4u; // uint4 per lane per chunk
+	constexpr bool EXT_HDR = !(PRE == PRE_NONE && ENC == ENC_RAW);
+	constexpr uint32_t HDR_BITS = EXT_HDR ? 176u : 128u;
+	__shared__ __attribute__((aligned(16))) uint32_t L[2][LWORDS];
+	__shared__ uint32_t s_wsum[CH][AIRS_WG / 64];
+	__shared__ uint32_t s_misc[8];
 
 	const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
 
-	if (tid == 0)
-		s_misc[0] = atomicAdd(a.ticket, 1u) - a.ticket_base;
-	__syncthreads();
-	const uint32_t seg = s_misc[0];
-	if (seg >= a.num_segs)
-		return; // grid == num_segs; defensive, uniform per workgroup
-
-	const uint32_t lf = seg / a.segs_per_frame;
-	const uint32_t sif = seg - lf * a.segs_per_frame;
+	// ---- segment id: dispatch order (or an atomic ticket, debug switch) ----
+	uint32_t seg = blockIdx.x;
+	if (a.dbg & 4u) {
+		if (tid == 0)
+			s_misc[0] = atomicAdd(a.ticket, 1u) - a.ticket_base;
+		__syncthreads();
+		seg = s_misc[0];
+	}
+	// Frame-interleaved dispatch: consecutive blocks take the same segment
+	// index of consecutive frames.  A frame's segments are still dispatched in
+	// order (a look-back only waits on earlier blocks) while the segments in
+	// flight spread over all frames, keeping each look-back chain short.
+	const uint32_t nfr = a.num_segs / a.segs_per_frame;
+	const uint32_t sif = seg / nfr;
+	const uint32_t lf = seg - sif * nfr;
+	const uint32_t gseg = lf * a.segs_per_frame + sif; // granule slot: frame-major
 	const uint32_t frame = a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul;
 	const bool is_first = sif == 0u;
 	const bool is_last = sif + 1u == a.segs_per_frame;
 	const uint32_t n = a.n;
 
-	const uint32_t gpar = a.frame_g ? a.frame_g[frame] : a.g;
-	const Coder c = make_coder<ENC>(ENC == ENC_RAW ? 1u : gpar, a.outlier_param);
-	const bool ext_hdr = !(a.pre_hdr == PRE_NONE && a.enc_hdr == ENC_RAW);
-	const uint32_t hdr_bits = ext_hdr ? 176u : 128u;
-
 	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
 	uint8_t *fmodel = nullptr;
-	if (a.model_mode != AIRS_MODEL_NONE)
+	if (MODEL)
 		fmodel = a.model_ptrs ? reinterpret_cast<uint8_t *>(a.model_ptrs[lf])
 				      : a.model + (uint64_t)(frame / a.model_div) * a.model_stride;
+	const bool src_al = ((uintptr_t)fsrc & 15u) == 0;
+	const bool mod_al = MODEL ? ((uintptr_t)fmodel & 15u) == 0 : true;
 
-	const uint32_t first = sif * AIRS_SEG + tid * AIRS_PT;
-	const uint32_t nv = first >= n ? 0u : min(n - first, (uint32_t)AIRS_PT);
-
-	uint32_t x[AIRS_PT];
-	load16<W>(fsrc, first, n, x);
-	uint32_t mo[AIRS_PT];
-	if (PRE == PRE_MODEL || a.model_mode == AIRS_MODEL_UPDATE)
-		load16_model(fmodel, first, n, mo);
-	else {
+	// ---- phase 0: issue every load of the segment -----------------------
+	uint32_t firstc[CH];
+	uint4 raw[CH][RW];
+	uint4 mraw[CH][2];
+	uint32_t prevld[CH];
 #pragma unroll
-		for (int j = 0; j < AIRS_PT; j++)
-			mo[j] = 0u;
-	}
-
-	// predecessor sample for DIFF (frame start: 0, i.e. r[0] = x[0])
-	uint32_t prev = 0u;
-	if (PRE == PRE_DIFF) {
-		prev = __shfl_up(x[AIRS_PT - 1], 1, 64);
-		if (lane == 0u) {
-			if (first == 0u || first > n)
-				prev = 0u;
-			else if (W == 2)
-				prev = reinterpret_cast<const uint16_t *>(fsrc)[first - 1u];
-			else
-				prev = reinterpret_cast<const uint32_t *>(fsrc)[first - 1u] & 0xFFFFu;
+	for (uint32_t c = 0; c < CH; c++) {
+		firstc[c] = sif * SEGN + c * AIRS_SEG + tid * AIRS_PT;
+		const bool full = firstc[c] + AIRS_PT <= n;
+		if (full && src_al) {
+			const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)firstc[c] * W);
+#pragma unroll
+			for (uint32_t q = 0; q < RW; q++)
+				raw[c][q] = p[q];
 		}
-	}
-
-	uint32_t cw1[AIRS_PT], l1[AIRS_PT], cw2[AIRS_PT], l2[AIRS_PT];
-	uint32_t T = 0u;
-#pragma unroll
-	for (int j = 0; j < AIRS_PT; j++) {
-		uint32_t u;
-		if (PRE == PRE_DIFF)
-			u = x[j] - (j ? x[j - 1] : prev);
-		else if (PRE == PRE_MODEL)
-			u = x[j] - mo[j];
-		else
-			u = x[j];
-		code_sample<ENC, RICE>(u & 0xFFFFu, c, cw1[j], l1[j], cw2[j], l2[j]);
-		if ((uint32_t)j >= nv) {
-			l1[j] = 0u;
-			l2[j] = 0u;
-			cw1[j] = 0u;
-			cw2[j] = 0u;
+		if (MODEL == 2 && full && mod_al) {
+			const uint4 *p = reinterpret_cast<const uint4 *>(fmodel + (size_t)firstc[c] * 2u);
+			mraw[c][0] = p[0];
+			mraw[c][1] = p[1];
 		}
-		T += l1[j] + l2[j];
+		prevld[c] = 0u;
+		if (PRE == PRE_DIFF && lane == 0u && firstc[c] != 0u && firstc[c] <= n)
+			prevld[c] = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fsrc)[firstc[c] - 1u]
+					   : reinterpret_cast<const uint32_t *>(fsrc)[firstc[c] - 1u] & 0xFFFFu;
 	}
 
-	// ---- block exclusive scan of per-lane bit counts -------------------
-	uint32_t inc = T;
-#pragma unroll
-	for (int d = 1; d < 64; d <<= 1) {
-		uint32_t y = __shfl_up(inc, d, 64);
-		if (lane >= (uint32_t)d)
-			inc += y;
-	}
-	if (lane == 63u)
-		s_misc[4 + wid] = inc;
-	__syncthreads();
-	uint32_t woff = 0u, A = 0u;
-#pragma unroll
-	for (uint32_t w = 0; w < AIRS_WG / 64; w++) {
-		uint32_t v = s_misc[4 + w];
-		woff += w < wid ? v : 0u;
-		A += v;
-	}
-	const uint32_t excl = woff + inc - T;
-
-	// ---- publish the aggregate as early as possible ---------------------
-	if (tid == 0) {
-		uint64_t tag = is_first ? ((uint64_t)a.epoch << 1 | 1u) : ((uint64_t)a.epoch << 1);
-		uint32_t val = is_first ? hdr_bits + A : A;
-		gran_store(&a.agg[seg], (tag << 32) | val);
-	}
-
-	// ---- pack the segment's bit stream into LDS (local bit 0 = L[0] MSB) --
-	const uint32_t nwords = (A + 31u) >> 5;
-	for (uint32_t i = tid; i <= nwords; i += AIRS_WG)
-		L[i] = 0u;
-	__syncthreads();
+	// zero both LDS chunk images while the loads are in flight
 	{
-		uint32_t wpos = excl >> 5, nb = excl & 31u;
+		uint4 *L4 = reinterpret_cast<uint4 *>(&L[0][0]);
+		for (uint32_t i = tid; i < 2u * LWORDS / 4u; i += AIRS_WG)
+			L4[i] = make_uint4(0u, 0u, 0u, 0u);
+	}
+
+	const uint32_t gpar = a.frame_g ? a.frame_g[frame] : a.g;
+	const Coder cd = make_coder<ENC>(ENC == ENC_RAW ? 1u : gpar, a.outlier_param);
+
+	// ---- phase 1: residuals, mapped values, code lengths ------------------
+	uint32_t mp[CH][AIRS_PT / 2]; // mapped values, two 16-bit per register
+	uint32_t nmp[MODEL ? CH : 1][AIRS_PT / 2]; // new model values (MODEL)
+	uint32_t T[CH], nv[CH];
+#pragma unroll
+	for (uint32_t c = 0; c < CH; c++) {
+		const uint32_t first = firstc[c];
+		nv[c] = first >= n ? 0u : min(n - first, (uint32_t)AIRS_PT);
+		uint32_t x[AIRS_PT];
+		if (nv[c] == AIRS_PT && src_al) {
+			if (W == 2) {
+				const uint32_t w8[8] = {raw[c][0].x, raw[c][0].y, raw[c][0].z, raw[c][0].w,
+							raw[c][1].x, raw[c][1].y, raw[c][1].z, raw[c][1].w};
+#pragma unroll
+				for (int j = 0; j < 8; j++) {
+					x[2 * j] = w8[j] & 0xFFFFu;
+					x[2 * j + 1] = w8[j] >> 16;
+				}
+			} else {
+#pragma unroll
+				for (uint32_t q = 0; q < 4; q++) {
+					x[4 * q + 0] = raw[c][q].x & 0xFFFFu;
+					x[4 * q + 1] = raw[c][q].y & 0xFFFFu;
+					x[4 * q + 2] = raw[c][q].z & 0xFFFFu;
+					x[4 * q + 3] = raw[c][q].w & 0xFFFFu;
+				}
+			}
+		} else {
+#pragma unroll
+			for (uint32_t j = 0; j < AIRS_PT; j++) {
+				const uint32_t i = first + j;
+				x[j] = i < n ? (W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fsrc)[i]
+						       : reinterpret_cast<const uint32_t *>(fsrc)[i] & 0xFFFFu)
+					     : 0u;
+			}
+		}
+		uint32_t mo[AIRS_PT];
+		if (MODEL == 2) {
+			if (nv[c] == AIRS_PT && mod_al) {
+				const uint32_t w8[8] = {mraw[c][0].x, mraw[c][0].y, mraw[c][0].z, mraw[c][0].w,
+							mraw[c][1].x, mraw[c][1].y, mraw[c][1].z, mraw[c][1].w};
+#pragma unroll
+				for (int j = 0; j < 8; j++) {
+					mo[2 * j] = w8[j] & 0xFFFFu;
+					mo[2 * j + 1] = w8[j] >> 16;
+				}
+			} else {
+#pragma unroll
+				for (uint32_t j = 0; j < AIRS_PT; j++)
+					mo[j] = first + j < n ? (uint32_t)reinterpret_cast<const uint16_t *>(fmodel)[first + j]
+							      : 0u;
+			}
+		}
+		uint32_t prev = 0u;
+		if (PRE == PRE_DIFF) {
+			prev = __shfl_up(x[AIRS_PT - 1], 1, 64);
+			if (lane == 0u)
+				prev = prevld[c];
+		}
+		uint32_t t = 0u;
+#pragma unroll
+		for (uint32_t j = 0; j < AIRS_PT; j++) {
+			uint32_t u;
+			if (PRE == PRE_DIFF)
+				u = x[j] - (j ? x[j - 1] : prev);
+			else if (PRE == PRE_MODEL)
+				u = x[j] - mo[j];
+			else
+				u = x[j];
+			u &= 0xFFFFu;
+			const uint32_t m = ENC == ENC_RAW ? u : zigzag16(u);
+			const uint32_t l = j < nv[c] ? len_from_m<ENC, RICE>(m, cd) : 0u;
+			t += l;
+			if (j & 1u)
+				mp[c][j >> 1] |= m << 16;
+			else
+				mp[c][j >> 1] = m;
+			if (MODEL) {
+				uint32_t nm;
+				if (MODEL == 1) {
+					nm = x[j];
+				} else {
+					const int32_t rate = (int32_t)a.model_rate;
+					const int32_t d = a.is_unsigned ? (int32_t)x[j] : (int32_t)(int16_t)x[j];
+					const int32_t mm = a.is_unsigned ? (int32_t)mo[j] : (int32_t)(int16_t)mo[j];
+					nm = (uint32_t)((mm * rate + d * (16 - rate)) >> 4) & 0xFFFFu;
+				}
+				if (j & 1u)
+					nmp[MODEL ? c : 0][j >> 1] |= nm << 16;
+				else
+					nmp[MODEL ? c : 0][j >> 1] = nm;
+			}
+		}
+		T[c] = t;
+		// Make the packed mapped values opaque: otherwise the compiler keeps
+		// phase 1's per-sample intermediates alive to CSE them with phase 2's
+		// recomputation, which costs ~100 extra VGPRs and halves occupancy.
+#pragma unroll
+		for (uint32_t i = 0; i < AIRS_PT / 2; i++)
+			asm volatile("" : "+v"(mp[c][i]));
+	}
+
+	// ---- per-chunk block scans (DPP within waves, LDS across waves) -------
+	uint32_t inc[CH];
+#pragma unroll
+	for (uint32_t c = 0; c < CH; c++) {
+		inc[c] = wave_incl_scan(T[c]);
+		if (lane == 63u)
+			s_wsum[c][wid] = inc[c];
+	}
+
+	// ---- the segment's last 32 bits (wave 3 rebuilds its last chunk) ------
+	uint64_t gv0 = 0;
+	__syncthreads(); // B1: wave totals visible
+	uint32_t excl[CH], tot[CH], base[CH];
+	uint32_t A = 0u;
+#pragma unroll
+	for (uint32_t c = 0; c < CH; c++) {
+		uint32_t woff = 0u, tt = 0u;
+#pragma unroll
+		for (uint32_t w = 0; w < AIRS_WG / 64; w++) {
+			const uint32_t v = s_wsum[c][w];
+			woff += w < wid ? v : 0u;
+			tt += v;
+		}
+		excl[c] = woff + inc[c] - T[c];
+		tot[c] = tt;
+		base[c] = A;
+		A += tt;
+	}
+	const uint32_t first_seg = gseg - sif;
+	if (wid == 0) {
+		if (lane == 0) {
+			const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
+			gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
+		}
+		if (!is_first && !(a.dbg & 2u)) {
+			const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane;
+			if (idx >= (int64_t)first_seg)
+				gv0 = gran_load(&a.agg[idx]);
+		}
+	}
+	if (!is_last && wid == AIRS_WG / 64 - 1) {
+		// lane 255 holds >= 16 bits of the last chunk; lane 254 supplies the rest
 		uint64_t acc = 0u;
 #pragma unroll
-		for (int j = 0; j < AIRS_PT; j++) {
-			acc = (acc << l1[j]) | cw1[j];
-			nb += l1[j];
-			if (nb >= 32u) {
-				nb -= 32u;
-				atomicOr(&L[wpos], (uint32_t)(acc >> nb));
-				wpos++;
-			}
-			if (ENC == ENC_MULTI) {
-				acc = (acc << l2[j]) | cw2[j];
-				nb += l2[j];
-				if (nb >= 32u) {
-					nb -= 32u;
-					atomicOr(&L[wpos], (uint32_t)(acc >> nb));
-					wpos++;
-				}
-			}
+		for (uint32_t j = 0; j < AIRS_PT; j++) {
+			const uint32_t m = (mp[CH - 1][j >> 1] >> (16u * (j & 1u))) & 0xFFFFu;
+			uint32_t c1, l1, c2, l2;
+			code_from_m<ENC, RICE>(m, cd, c1, l1, c2, l2);
+			acc = (acc << l1) | c1;
+			if (NPIECE == 2)
+				acc = (acc << l2) | c2;
 		}
-		if (nb && T)
-			atomicOr(&L[wpos], (uint32_t)(acc << (32u - nb)));
-	}
-	__syncthreads();
-
-	// ---- publish the last 32 bits of the segment for the successor -------
-	if (tid == 0 && !is_last) {
-		const uint32_t s0 = A - 32u, q = s0 >> 5, r = s0 & 31u;
-		const uint32_t t32 = r ? (L[q] << r) | (L[q + 1] >> (32u - r)) : L[q];
-		gran_store(&a.tail[seg], ((uint64_t)a.epoch << 32) | t32);
+		const uint32_t lo = (uint32_t)acc;
+		const uint32_t lo_prev = __shfl_up(lo, 1, 64);
+		if (lane == 63u) {
+			const uint32_t tl = T[CH - 1];
+			const uint32_t t32 = tl >= 32u ? lo : ((lo_prev << tl) | (lo & ((1u << tl) - 1u)));
+			gran_store(&a.tail[gseg], ((uint64_t)a.epoch << 32) | t32);
+		}
 	}
 
-	// ---- decoupled look-back (wave 0) ------------------------------------
-	if (wid == 0) {
-		uint32_t P = hdr_bits;
-		if (!is_first) {
-			const uint32_t first_seg = seg - sif;
-			uint32_t sum = 0u, spins = 0u;
-			int64_t j = (int64_t)seg - 1;
-			for (;;) {
-				const int64_t idx = j - (int64_t)lane;
-				const bool inr = idx >= (int64_t)first_seg;
-				const uint64_t gv = inr ? gran_load(&a.agg[idx]) : 0ull;
-				const uint32_t tag = (uint32_t)(gv >> 32);
-				const bool valid = inr && (tag >> 1) == a.epoch;
-				const bool incl = valid && (tag & 1u);
-				const uint64_t incl_m = __ballot(incl);
-				const uint64_t bad_m = __ballot(inr && !valid);
-				const uint32_t fi = incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
-				const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
-				if (bad_m & need) {
-					if (++spins > AIRS_SPIN_LIMIT) {
-						// never expected: a predecessor did not publish.  Give up
-						// (output is garbage, the host reports the fault counter)
-						if (lane == 0)
-							atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-						break;
-					}
-					__builtin_amdgcn_s_sleep(1);
-					continue;
-				}
-				uint32_t v = (inr && lane <= fi) ? (uint32_t)gv : 0u;
+	uint32_t last_ne = 0u; // last non-empty chunk
 #pragma unroll
-				for (int d = 32; d >= 1; d >>= 1)
-					v += __shfl_xor(v, d, 64);
-				sum += v;
-				if (incl_m)
-					break;
-				j -= 64;
-			}
-			P = sum;
-			if (lane == 0)
-				gran_store(&a.agg[seg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (P + A));
-		}
-		if (lane == 0) {
-			uint32_t pred = 0u;
-			if (is_first) {
-				// header bytes 20-21 (low 16 bits of the outlier field) share
-				// the first payload dword of a 22-byte header
-				pred = (ext_hdr && ENC != ENC_RAW) ? (c.outlier & 0xFFFFu) : 0u;
-			} else {
-				uint64_t tv;
-				for (uint32_t spins = 0;; spins++) {
-					tv = gran_load(&a.tail[seg - 1u]);
-					if ((uint32_t)(tv >> 32) == a.epoch)
-						break;
-					if (spins > AIRS_SPIN_LIMIT) {
-						atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-						break;
-					}
-					__builtin_amdgcn_s_sleep(1);
-				}
-				pred = (uint32_t)tv;
-			}
-			s_misc[1] = P;
-			s_misc[2] = pred;
-		}
-	}
-	__syncthreads();
+	for (uint32_t c = 0; c < CH; c++)
+		last_ne = tot[c] ? c : last_ne;
 
-	// ---- store: funnel-shift the LDS image to the frame bit offset --------
-	const uint32_t P = s_misc[1];
-	const uint32_t pred = s_misc[2];
-	const uint32_t r = P & 31u, g0 = P >> 5;
-	const uint32_t endbit = P + A;
-	const uint32_t J = ((endbit - 1u) >> 5) - g0; // words touched: g0 .. g0+J
-	const bool last_complete = (endbit & 31u) == 0u;
 	uint8_t *fdst = a.dst + (uint64_t)frame * a.dst_stride;
 	const uint32_t cap = a.cap;
-	for (uint32_t j = tid; j <= J; j += AIRS_WG) {
-		const uint32_t hi = j ? L[j - 1u] : pred;
-		const uint32_t v = __builtin_amdgcn_alignbit(hi, L[j], r);
-		const uint32_t gw = g0 + j;
-		if (j < J || last_complete) {
-			if (4u * gw + 4u <= cap)
-				*reinterpret_cast<uint32_t *>(fdst + 4u * gw) = bswap32(v);
-		} else if (is_last) {
-			// zero-padded final bytes of the payload (reference bitstream_flush)
-			const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
-			for (uint32_t b = 0; b < nbytes; b++)
-				if (4u * gw + b < cap)
-					fdst[4u * gw + b] = (uint8_t)(v >> (24u - 8u * b));
+	uint32_t P = 0u;
+	uint32_t pred_c = 0u; // (lane 0 of wave 0) bits preceding chunk c in its first dword
+
+	// ---- phase 2: chunk by chunk: codewords -> LDS image -> HBM -----------
+	// rolled loop (keeps register pressure flat): the current chunk's state is
+	// always index 0 of mp/nmp/nv/excl/tot/base/firstc, rotated at the end
+	uint32_t tot_m2 = 0u; // total of chunk c-2 (its image is recycled now)
+	uint32_t tot_m1 = 0u;
+#pragma unroll 1
+	for (uint32_t c = 0; c < CH; c++) {
+		uint32_t *Lc = L[c & 1u];
+		if (c >= 2) {
+			// image c&1 was last read by chunk c-2's stores (before the barrier
+			// that ended chunk c-1's packing): clear what it used
+			const uint32_t nw = (max(tot_m2, tot[0]) + 31u) >> 5;
+			for (uint32_t i = tid; i <= nw; i += AIRS_WG)
+				Lc[i] = 0u;
+			__syncthreads();
+		}
+		uint32_t cw[NPIECE][AIRS_PT], ln[NPIECE][AIRS_PT];
+#pragma unroll
+		for (uint32_t j = 0; j < AIRS_PT; j++) {
+			const uint32_t m = (mp[0][j >> 1] >> (16u * (j & 1u))) & 0xFFFFu;
+			uint32_t c1, l1, c2, l2;
+			code_from_m<ENC, RICE>(m, cd, c1, l1, c2, l2);
+			const bool ok = j < nv[0];
+			cw[0][j] = ok ? c1 : 0u;
+			ln[0][j] = ok ? l1 : 0u;
+			if (NPIECE == 2) {
+				cw[NPIECE - 1][j] = ok ? c2 : 0u;
+				ln[NPIECE - 1][j] = ok ? l2 : 0u;
+			}
+		}
+		{
+			uint32_t wpos = excl[0] >> 5, nb = excl[0] & 31u;
+			uint64_t acc = 0u;
+#pragma unroll
+			for (uint32_t j = 0; j < AIRS_PT; j++) {
+#pragma unroll
+				for (uint32_t p = 0; p < NPIECE; p++) {
+					acc = (acc << ln[p][j]) | cw[p][j];
+					nb += ln[p][j];
+					const bool e = nb >= 32u;
+					nb -= e ? 32u : 0u;
+					// branch-free: OR 0 into the current word when nothing completed
+					atomicOr(&Lc[wpos], e ? (uint32_t)(acc >> nb) : 0u);
+					wpos += e ? 1u : 0u;
+				}
+			}
+			if (nb)
+				atomicOr(&Lc[wpos], (uint32_t)(acc << (32u - nb)));
+		}
+		__syncthreads();
+		uint32_t pred_next = 0u; // last 32 bits of this chunk, for chunk c+1 (tid 0)
+		if (c + 1u < CH && tid == 0 && tot[0] >= 32u) {
+			const uint32_t s0 = tot[0] - 32u, q = s0 >> 5, sh = s0 & 31u;
+			pred_next = sh ? (Lc[q] << sh) | (Lc[q + 1] >> (32u - sh)) : Lc[q];
+		}
+
+		if (c == 0) {
+			// ---- decoupled look-back (wave 0), overlapped with the packing ----
+			if (wid == 0) {
+				uint32_t Pw = HDR_BITS;
+				if (a.dbg & 2u) {
+					Pw = HDR_BITS + sif * 37u; // ablation: no look-back (output garbage)
+				} else if (!is_first) {
+					// round 0 uses the 64 granules fetched before packing; later
+					// rounds fetch LB_WIN windows of 64 at once, newest first
+					constexpr int LB_WIN = 4;
+					uint32_t sum = 0u, spins = 0u;
+					int64_t j = (int64_t)gseg - 1;
+					uint64_t gv[LB_WIN];
+					int nwin = 1;
+					gv[0] = gv0;
+#pragma unroll
+					for (int w = 1; w < LB_WIN; w++)
+						gv[w] = 0;
+					bool done = false;
+					while (!done) {
+						bool retry = false;
+#pragma unroll
+						for (int w = 0; w < LB_WIN; w++) {
+							if (w >= nwin || done || retry)
+								break;
+							const int64_t idx = j - 64 * w - (int64_t)lane;
+							const bool inr = idx >= (int64_t)first_seg;
+							const uint32_t tag = (uint32_t)(gv[w] >> 32);
+							const bool valid = inr && (tag >> 1) == a.epoch;
+							const bool incl = valid && (tag & 1u);
+							const uint64_t incl_m = __ballot(incl);
+							const uint64_t bad_m = __ballot(inr && !valid);
+							const uint32_t fi =
+								incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
+							const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
+							if (bad_m & need) {
+								// a needed predecessor has not published: re-poll from here
+								j -= 64 * w;
+								retry = true;
+								break;
+							}
+							sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv[w] : 0u);
+							if (incl_m)
+								done = true;
+						}
+						if (done)
+							break;
+						if (retry) {
+							if (++spins > AIRS_SPIN_LIMIT) {
+								// never expected: a predecessor did not publish.  Give up
+								// (output is garbage, the host reports the fault counter)
+								if (lane == 0)
+									atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+								break;
+							}
+							__builtin_amdgcn_s_sleep(1);
+						} else {
+							j -= 64 * nwin;
+						}
+						nwin = LB_WIN;
+#pragma unroll
+						for (int w = 0; w < LB_WIN; w++) {
+							const int64_t idx = j - 64 * w - (int64_t)lane;
+							gv[w] = idx >= (int64_t)first_seg ? gran_load(&a.agg[idx]) : 0ull;
+						}
+					}
+					Pw = sum;
+					if (lane == 0)
+						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (Pw + A));
+				}
+				if (lane == 0) {
+					uint32_t pred = 0u;
+					if (is_first || (a.dbg & 2u)) {
+						// header bytes 20-21 (low half of the outlier field) share
+						// the first payload dword of a 22-byte header
+						pred = (EXT_HDR && ENC != ENC_RAW) ? (cd.outlier & 0xFFFFu) : 0u;
+					} else {
+						uint64_t tv;
+						for (uint32_t spins = 0;; spins++) {
+							tv = gran_load(&a.tail[gseg - 1u]);
+							if ((uint32_t)(tv >> 32) == a.epoch)
+								break;
+							if (spins > AIRS_SPIN_LIMIT) {
+								atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+								break;
+							}
+							__builtin_amdgcn_s_sleep(1);
+						}
+						pred = (uint32_t)tv;
+					}
+					s_misc[1] = Pw;
+					s_misc[2] = pred;
+				}
+			}
+			__syncthreads();
+			P = s_misc[1];
+			pred_c = s_misc[2];
+		}
+
+		// ---- store chunk c: funnel-shift the image to its frame bit offset ----
+		if (tot[0]) {
+			const uint32_t Pc = P + base[0];
+			const uint32_t r = Pc & 31u, g0 = Pc >> 5;
+			const uint32_t endbit = Pc + tot[0];
+			const uint32_t J = ((endbit - 1u) >> 5) - g0;
+			const bool last_complete = (endbit & 31u) == 0u;
+			const bool final_chunk = is_last && c == last_ne;
+			for (uint32_t j = tid; j <= J; j += AIRS_WG) {
+				uint32_t hi;
+				if (j)
+					hi = Lc[j - 1u];
+				else
+					hi = pred_c;
+				const uint32_t v = __builtin_amdgcn_alignbit(hi, Lc[j], r);
+				const uint32_t gw = g0 + j;
+				if (j < J || last_complete) {
+					if (4u * gw + 4u <= cap)
+						*reinterpret_cast<uint32_t *>(fdst + 4u * gw) = bswap32(v);
+				} else if (final_chunk) {
+					// zero-padded final bytes of the payload (reference bitstream_flush)
+					const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
+					for (uint32_t b = 0; b < nbytes; b++)
+						if (4u * gw + b < cap)
+							fdst[4u * gw + b] = (uint8_t)(v >> (24u - 8u * b));
+				}
+			}
+		}
+
+		// ---- model update of chunk c (cmp.c:304-311), old model kept for the
+		// samples the reference's loop never reached (see fail_bit) ----------
+		if (MODEL && nv[0]) {
+			uint64_t bpos = (uint64_t)P + base[0] + excl[0];
+			bool all_ok = true;
+			uint32_t okmask = 0u;
+#pragma unroll
+			for (uint32_t j = 0; j < AIRS_PT; j++) {
+#pragma unroll
+				for (uint32_t p = 0; p < NPIECE; p++)
+					bpos += ln[p][j];
+				const bool ok = j < nv[0] && bpos <= a.fail_bit;
+				okmask |= ok ? (1u << j) : 0u;
+				all_ok &= ok;
+			}
+			uint16_t *mpp = reinterpret_cast<uint16_t *>(fmodel) + firstc[0];
+			if (all_ok && mod_al) {
+				const uint32_t *q = nmp[0];
+				reinterpret_cast<uint4 *>(mpp)[0] = make_uint4(q[0], q[1], q[2], q[3]);
+				reinterpret_cast<uint4 *>(mpp)[1] = make_uint4(q[4], q[5], q[6], q[7]);
+			} else {
+#pragma unroll
+				for (uint32_t j = 0; j < AIRS_PT; j++)
+					if (okmask & (1u << j))
+						mpp[j] = (uint16_t)(nmp[0][j >> 1] >> (16u * (j & 1u)));
+			}
+		}
+		pred_c = pred_next;
+		// rotate the per-chunk state
+		tot_m2 = tot_m1;
+		tot_m1 = tot[0];
+#pragma unroll
+		for (uint32_t k = 0; k + 1 < CH; k++) {
+#pragma unroll
+			for (uint32_t i = 0; i < AIRS_PT / 2; i++) {
+				mp[k][i] = mp[k + 1][i];
+				if (MODEL)
+					nmp[k][i] = nmp[k + 1][i];
+			}
+			nv[k] = nv[k + 1];
+			excl[k] = excl[k + 1];
+			tot[k] = tot[k + 1];
+			base[k] = base[k + 1];
+			firstc[k] = firstc[k + 1];
 		}
 	}
 
 	// ---- frame epilogue: checksum, header, status ------------------------
 	if (is_last && tid == 0) {
+		const uint32_t endbit = P + A;
 		const uint32_t payload_bytes = (endbit + 7u) >> 3;
 		const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
 		if (a.checksum) {
@@ -507,18 +808,15 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 					fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
 		}
 		const uint64_t id = a.ids ? a.ids[lf] : a.id_base + (uint64_t)lf * a.id_step;
-		uint8_t h[24];
-		header_bytes(h, size, 2u * n, id, a.seq, PRE, a.checksum ? 1u : 0u, ENC,
-			     PRE == PRE_MODEL ? a.model_rate_hdr : 0u, ENC == ENC_RAW ? 0u : gpar,
-			     ENC == ENC_RAW ? 0u : c.outlier);
-		const uint32_t hwords = ext_hdr ? 5u : 4u; // bytes 20-21 travel with the payload
-		for (uint32_t w = 0; w < hwords; w++) {
-			if (4u * w + 4u <= cap) {
-				uint32_t v = ((uint32_t)h[4 * w] << 24) | ((uint32_t)h[4 * w + 1] << 16) |
-					     ((uint32_t)h[4 * w + 2] << 8) | h[4 * w + 3];
-				*reinterpret_cast<uint32_t *>(fdst + 4u * w) = bswap32(v);
-			}
-		}
+		uint32_t h[5];
+		header_words(h, size, 2u * n, id, a.seq, PRE, a.checksum ? 1u : 0u, ENC,
+			     PRE == PRE_MODEL ? a.model_rate : 0u, ENC == ENC_RAW ? 0u : gpar,
+			     ENC == ENC_RAW ? 0u : cd.outlier);
+		const uint32_t hwords = EXT_HDR ? 5u : 4u;
+#pragma unroll
+		for (uint32_t w = 0; w < 5u; w++)
+			if (w < hwords && 4u * w + 4u <= cap)
+				*reinterpret_cast<uint32_t *>(fdst + 4u * w) = bswap32(h[w]);
 		uint32_t st = size;
 		if (size > cap)
 			st = ERRV(E_DST_TOO_SMALL);
@@ -527,48 +825,6 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		a.status[frame] = st;
 		if (a.needed)
 			a.needed[frame] = size;
-	}
-
-	// ---- model update, after the frame offset is known (cmp.c:304-311) ----
-	if (a.model_mode != AIRS_MODEL_NONE && nv) {
-		uint32_t nm[AIRS_PT];
-		uint64_t bpos = (uint64_t)P + excl;
-		bool all_ok = true;
-		uint32_t okmask = 0u;
-		const int32_t rate = (int32_t)a.model_rate;
-#pragma unroll
-		for (int j = 0; j < AIRS_PT; j++) {
-			bpos += l1[j] + l2[j];
-			const bool ok = (uint32_t)j < nv && bpos <= a.fail_bit;
-			okmask |= ok ? (1u << j) : 0u;
-			all_ok &= ok;
-			if (a.model_mode == AIRS_MODEL_STORE) {
-				nm[j] = x[j];
-			} else {
-				int32_t d = a.is_unsigned ? (int32_t)x[j] : (int32_t)(int16_t)x[j];
-				int32_t m = a.is_unsigned ? (int32_t)mo[j] : (int32_t)(int16_t)mo[j];
-				nm[j] = (uint32_t)((m * rate + d * (16 - rate)) >> 4) & 0xFFFFu;
-			}
-		}
-		uint16_t *mp = reinterpret_cast<uint16_t *>(fmodel) + first;
-		if (all_ok && ((uintptr_t)fmodel & 15u) == 0) {
-			uint4 v0, v1;
-			v0.x = nm[0] | (nm[1] << 16);
-			v0.y = nm[2] | (nm[3] << 16);
-			v0.z = nm[4] | (nm[5] << 16);
-			v0.w = nm[6] | (nm[7] << 16);
-			v1.x = nm[8] | (nm[9] << 16);
-			v1.y = nm[10] | (nm[11] << 16);
-			v1.z = nm[12] | (nm[13] << 16);
-			v1.w = nm[14] | (nm[15] << 16);
-			reinterpret_cast<uint4 *>(mp)[0] = v0;
-			reinterpret_cast<uint4 *>(mp)[1] = v1;
-		} else {
-#pragma unroll
-			for (int j = 0; j < AIRS_PT; j++)
-				if (okmask & (1u << j))
-					mp[j] = (uint16_t)nm[j];
-		}
 	}
 }
 
@@ -887,47 +1143,50 @@ static uint32_t ensure_granules(airs_dev_engine *e, size_t segs)
 	return 0;
 }
 
-template <int W, int PRE, int ENC, bool RICE>
+template <int W, int PRE, int ENC, bool RICE, int MODEL>
 static void launch_encode(const KArgs &k, uint32_t grid, hipStream_t s)
 {
-	hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE>), dim3(grid), dim3(AIRS_WG), 0, s, k);
+	hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL>), dim3(grid), dim3(AIRS_WG), 0, s, k);
 }
 
-template <int W, int PRE>
+template <int W, int PRE, int MODEL>
 static void dispatch_enc(const KArgs &k, uint32_t enc, bool rice, uint32_t grid, hipStream_t s)
 {
 	switch (enc) {
 	case ENC_RAW:
-		launch_encode<W, PRE, ENC_RAW, true>(k, grid, s);
+		launch_encode<W, PRE, ENC_RAW, true, MODEL>(k, grid, s);
 		break;
 	case ENC_ZERO:
 		if (rice)
-			launch_encode<W, PRE, ENC_ZERO, true>(k, grid, s);
+			launch_encode<W, PRE, ENC_ZERO, true, MODEL>(k, grid, s);
 		else
-			launch_encode<W, PRE, ENC_ZERO, false>(k, grid, s);
+			launch_encode<W, PRE, ENC_ZERO, false, MODEL>(k, grid, s);
 		break;
 	default:
 		if (rice)
-			launch_encode<W, PRE, ENC_MULTI, true>(k, grid, s);
+			launch_encode<W, PRE, ENC_MULTI, true, MODEL>(k, grid, s);
 		else
-			launch_encode<W, PRE, ENC_MULTI, false>(k, grid, s);
+			launch_encode<W, PRE, ENC_MULTI, false, MODEL>(k, grid, s);
 		break;
 	}
 }
 
 template <int W>
-static void dispatch_pre(const KArgs &k, uint32_t pre, uint32_t enc, bool rice, uint32_t grid, hipStream_t s)
+static void dispatch_pre(const KArgs &k, uint32_t pre, uint32_t enc, bool rice, uint32_t model_mode,
+			 uint32_t grid, hipStream_t s)
 {
-	switch (pre) {
-	case PRE_NONE:
-		dispatch_enc<W, PRE_NONE>(k, enc, rice, grid, s);
-		break;
-	case PRE_DIFF:
-		dispatch_enc<W, PRE_DIFF>(k, enc, rice, grid, s);
-		break;
-	default:
-		dispatch_enc<W, PRE_MODEL>(k, enc, rice, grid, s);
-		break;
+	if (pre == PRE_MODEL) {
+		dispatch_enc<W, PRE_MODEL, AIRS_MODEL_UPDATE>(k, enc, rice, grid, s);
+	} else if (pre == PRE_DIFF) {
+		if (model_mode == AIRS_MODEL_STORE)
+			dispatch_enc<W, PRE_DIFF, AIRS_MODEL_STORE>(k, enc, rice, grid, s);
+		else
+			dispatch_enc<W, PRE_DIFF, AIRS_MODEL_NONE>(k, enc, rice, grid, s);
+	} else {
+		if (model_mode == AIRS_MODEL_STORE)
+			dispatch_enc<W, PRE_NONE, AIRS_MODEL_STORE>(k, enc, rice, grid, s);
+		else
+			dispatch_enc<W, PRE_NONE, AIRS_MODEL_NONE>(k, enc, rice, grid, s);
 	}
 }
 
@@ -939,7 +1198,8 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 		return ERRV(E_PARAMS_INVALID);
 	if (L->encoder_type > ENC_MULTI || (L->sample_bytes != 2 && L->sample_bytes != 4))
 		return ERRV(E_PARAMS_INVALID);
-	const uint32_t spf = (L->n + AIRS_SEG - 1) / AIRS_SEG;
+	const uint32_t segn = seg_chunks(L->sample_bytes == 4 ? 4 : 2, L->model_mode ? 1 : 0) * AIRS_SEG;
+	const uint32_t spf = (L->n + segn - 1) / segn;
 	const uint64_t segs = (uint64_t)spf * L->num_frames;
 	if (segs > 0x7FFFFFFFull)
 		return ERRV(E_PARAMS_INVALID);
@@ -990,15 +1250,26 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	if (e->epoch == 0)
 		e->epoch = 1;
 	k.epoch = e->epoch;
+	{
+		static int dbg = -1;
+		if (dbg < 0) {
+			const char *v = getenv("AIRS_DBG");
+			dbg = v ? atoi(v) : 0;
+		}
+		k.dbg = (uint32_t)dbg;
+	}
 
 	bool rice = L->frame_g != nullptr ||
 		    (L->encoder_param && (L->encoder_param & (L->encoder_param - 1u)) == 0u);
+	if (L->preprocessing == PRE_MODEL && L->model_mode != AIRS_MODEL_UPDATE)
+		return ERRV(E_PARAMS_INVALID);
 	if (L->sample_bytes == 2)
-		dispatch_pre<2>(k, L->preprocessing, L->encoder_type, rice, (uint32_t)segs, e->stream);
+		dispatch_pre<2>(k, L->preprocessing, L->encoder_type, rice, L->model_mode, (uint32_t)segs, e->stream);
 	else
-		dispatch_pre<4>(k, L->preprocessing, L->encoder_type, rice, (uint32_t)segs, e->stream);
+		dispatch_pre<4>(k, L->preprocessing, L->encoder_type, rice, L->model_mode, (uint32_t)segs, e->stream);
 	HIPCHECK(hipGetLastError());
-	e->ticket_base += (uint32_t)segs;
+	if (k.dbg & 4u)
+		e->ticket_base += (uint32_t)segs;
 	return 0;
 }
 
