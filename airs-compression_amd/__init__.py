@@ -136,3 +136,11 @@ class GpuEngine:
 
 def context_array(n: int):
     return (CmpContext * n)()
+
+
+def __getattr__(name):
+    # submodules that need torch are imported on first use
+    if name == "shard":
+        import importlib
+        return importlib.import_module(__name__ + ".shard")
+    raise AttributeError(name)

@@ -56,6 +56,20 @@ WORKLOADS = {
 PARAMS = dict(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=32)
 
 
+def measured_traffic(wname):
+    """HBM bytes per launch of the encode kernel from the latest committed
+    PMC passes (profiles/rNN_traffic_<workload>.json, written by
+    scripts/traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE runs of this
+    bench command), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{wname}.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        t = json.load(f)
+    return t.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def frame_ids(wl, rank, world):
     if wl["layout"] == "roundrobin":
         return [rank + world * j for j in range(wl["frames"])]
@@ -98,12 +112,15 @@ def cpu_baseline(wl, threads):
         return dt
 
     run(threads)  # warm-up
-    best = min(run(threads) for _ in range(3))
+    times = sorted(run(threads) for _ in range(5))
+    best = times[0]
     single = run(1) if nf <= 16 else None
     nbytes = nf * 2 * n
     out = dict(value=round(nbytes / best / 1e9, 4), unit="GB/s", cores=threads, kind=kind,
-               sample=f"{nf} frames x {n} u16 samples ({nbytes / 2**20:.0f} MiB, the same synthetic frames), "
-                      f"best of 3 after a warm-up, OpenMP over frames")
+               sample=f"{nf} frames x {n} u16 samples ({nbytes / 2**20:.0f} MiB, the same synthetic frames "
+                      f"and parameters), best of 5 after a warm-up, OpenMP over frames, one context per "
+                      f"thread; host has {os.cpu_count()} logical CPUs",
+               median_value=round(nbytes / times[2] / 1e9, 4))
     if single is not None:
         out["single_thread_value"] = round(nbytes / single / 1e9, 4)
     return out
@@ -218,15 +235,31 @@ def main():
     # ---- gather of compressed frames to rank 0 over RCCL (not in `value`) --
     gather = None
     if world > 1 and not args.no_gather:
-        shard = pkg.shard
-        gstats = shard.gather_frames_timed(dist, dst, dstride, sizes, nf, rank, world, lib=lib, eng=eng)
-        gather = gstats
+        layout = "roundrobin" if wl["layout"] == "roundrobin" else "block"
+        gather, g = pkg.shard.gather_frames_timed(dist, dst, dstride, sizes, nf, rank, world, layout=layout,
+                                                  patch_base=0)
+        if g is not None:
+            host_all = g.data.cpu().numpy()
+            offs, lens = g.offsets.numpy(), g.sizes.numpy()
+            hg = hashlib.sha256()
+            for f in range(g.num_frames):
+                b = bytearray(host_all[offs[f]:offs[f] + lens[f]])
+                ok_id = int.from_bytes(b[8:14], "big") == 1 + f
+                b[8:14] = b"\0" * 6
+                hg.update(b)
+                if not ok_id:
+                    gather["identifier_patch_ok"] = False
+            gather.setdefault("identifier_patch_ok", True)
+            gwant = gold.get(f"gather_digest_n{world}") if wl["layout"] == "roundrobin" else None
+            gather["bitexact_vs_reference"] = (hg.hexdigest() == gwant) if gwant else None
+            del g, host_all
 
     in_bytes_rank = nf * 2 * n
     total_in = in_bytes_rank * world
     value = total_in * args.steps / wall_max / 1e9
     ms_step = wall_max / args.steps * 1e3
     kern_avg_ms = float(np.mean(kern_ms))
+    traffic, traffic_src = measured_traffic(wname)
     achieved = in_bytes_rank / (kern_avg_ms * 1e-3) / 1e9
     result = None
     if rank == 0:
@@ -264,7 +297,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "airs::encode_kernel<2,1,1,true> (u16, DIFF, GOLOMB_ZERO, Rice)",
                 "algorithmic_bytes_per_launch": in_bytes_rank,
                 "avg_launch_ms_hip_events": round(kern_avg_ms, 5),

@@ -147,6 +147,8 @@ def reference_digest(name, lib_path):
         # bench.py shards: rank r of N encodes frames r + N*j, j < 1024
         for nw in (1, 2, 4, 8):
             d[f"shard_digests_n{nw}"] = [frame_digest(frames[r::nw][:1024])["digest"] for r in range(nw)]
+            # what rank 0 holds after gathering N shards: frames 0 .. 1024*N-1 in f order
+            d[f"gather_digest_n{nw}"] = frame_digest(frames[:1024 * nw])["digest"]
     if gs is not None:
         d["rice_g_digest"] = hashlib.sha256(np.array(gs, dtype=np.uint32).tobytes()).hexdigest()
     return d

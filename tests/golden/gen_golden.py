@@ -200,42 +200,37 @@ def check_kat_claims(kat, results):
         assert results[i]["frame"] == want, (kat["name"], i, results[i]["frame"])
 
 
-def main():
-    ref = api.CmpLib(REF_PATH)
-    orc = api.CmpLib(ORC_PATH)
-    only_cfg = "--configs-only" in sys.argv
-    # --- KATs ---
+def gen_kats(ref, orc):
     out = []
-    for kat in ([] if only_cfg else KATS):
+    for kat in KATS:
         res = run_kat(ref, kat)
         check_kat_claims(kat, res)
         assert run_kat(orc, kat) == res, kat["name"]
         k = dict(kat)
         k["expected"] = res
         out.append(k)
-    if not only_cfg:
-      with open(os.path.join(HERE, "kats.json"), "w") as f:
+    with open(os.path.join(HERE, "kats.json"), "w") as f:
         json.dump(dict(generator="tests/golden/gen_golden.py", produced_by="oracle/_ref/libref.so",
                        cases=out), f, indent=1)
-    if not only_cfg:
-      print("kats:", len(out))
+    print("kats:", len(out))
 
-    # --- random scenario digests ---
+
+def gen_random(ref):
     seqs = []
-    for trial in (range(0) if only_cfg else range(400)):
+    for trial in range(400):
         params, kind, n = scenarios.random_case(api.CmpParams, trial, allow_iwt=True)
         res = scenarios.run_sequence(ref, params, kind, n, seed=trial)
         seqs.append(dict(trial=trial, kind=kind, n=n, params=params.as_dict(),
                          digest=hashlib.sha256(repr(res).encode()).hexdigest(),
                          ok_frames=sum(1 for x in res[1:] if not api.is_error(x[0]))))
-    if not only_cfg:
-      with open(os.path.join(HERE, "random_sequences.json"), "w") as f:
+    with open(os.path.join(HERE, "random_sequences.json"), "w") as f:
         json.dump(dict(generator="tests/golden/gen_golden.py", produced_by="oracle/_ref/libref.so",
                        note="digest = sha256(repr(tests.scenarios.run_sequence(lib, ...)))", cases=seqs), f,
                   indent=0)
     print("random sequences:", len(seqs), "ok frames:", sum(s["ok_frames"] for s in seqs))
 
-    # --- BASELINE config digests ---
+
+def gen_configs():
     import configs as cfgmod
     res = {}
     for name in cfgmod.CONFIGS:
@@ -245,6 +240,19 @@ def main():
         json.dump(dict(generator="tests/golden/gen_golden.py", produced_by="oracle/_ref/libref.so",
                        note="sha256 over frames in order with header identifier bytes 8..13 zeroed",
                        configs=res), f, indent=1)
+
+
+def main():
+    """usage: gen_golden.py [kats] [random] [configs]   (default: all three)"""
+    stages = [a for a in sys.argv[1:] if not a.startswith("-")] or ["kats", "random", "configs"]
+    ref = api.CmpLib(REF_PATH)
+    orc = api.CmpLib(ORC_PATH)
+    if "kats" in stages:
+        gen_kats(ref, orc)
+    if "random" in stages:
+        gen_random(ref)
+    if "configs" in stages:
+        gen_configs()
 
 
 if __name__ == "__main__":
