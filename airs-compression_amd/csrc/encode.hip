@@ -289,6 +289,88 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 	return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
 }
 
+// Two 16-bit lanes per VGPR (v_pk_* ops): samples, residuals and mapped
+// values of a lane's 16 samples travel as 8 packed registers.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 pk(uint32_t x)
+{
+	return __builtin_bit_cast(u16x2, x);
+}
+
+__device__ __forceinline__ uint32_t unpk(u16x2 x)
+{
+	return __builtin_bit_cast(uint32_t, x);
+}
+
+__device__ __forceinline__ uint32_t half16(uint32_t w, uint32_t h)
+{
+	return h ? w >> 16 : w & 0xFFFFu;
+}
+
+// ZigZag of two 16-bit residuals at once (reference encoder.c:274-286)
+__device__ __forceinline__ uint32_t zigzag_pk(uint32_t u)
+{
+	const u16x2 x = pk(u);
+	return unpk((x << (u16x2)(1)) ^ __builtin_bit_cast(u16x2, __builtin_bit_cast(i16x2, x) >> (i16x2)(15)));
+}
+
+// Rice/ZERO pair terms: v = m + 1 saturated at 0xFFFF (exact for k <= 11,
+// where m = 0xFFFF escapes either way), q = v >> k, low = v & (2^k - 1)
+struct RicePair {
+	uint32_t q, low, lq; // packed; lq = min(q, 16)
+};
+
+__device__ __forceinline__ RicePair rice_pair(uint32_t m2, uint32_t k, uint32_t mask)
+{
+	const u16x2 v = __builtin_elementwise_add_sat(pk(m2), (u16x2)(1));
+	const u16x2 q = v >> (u16x2)((unsigned short)k);
+	RicePair r;
+	r.q = unpk(q);
+	r.low = unpk(v & (u16x2)((unsigned short)mask));
+	r.lq = unpk(__builtin_elementwise_min(q, (u16x2)(16)));
+	return r;
+}
+
+// Bit packer into an LDS image.  `nb` is the absolute bit position inside
+// the image; acc holds (at least) the last 32 + (nb mod 32) bits.  Every put
+// ORs the 32 bits that precede the pending ones into their word: when a word
+// just completed that is the new word, otherwise it is the previous word
+// again (or zeros before the lane's first bit), which ORs nothing new.  So
+// there is one ds_or per piece and no select or branch.
+struct Packer {
+	uint64_t acc;
+	uint32_t nb;
+	uint32_t *img;
+
+	__device__ __forceinline__ void init(uint32_t *image, uint32_t bit)
+	{
+		acc = 0u;
+		nb = bit;
+		img = image;
+	}
+	__device__ __forceinline__ void put(uint32_t cw, uint32_t len) // len <= 32, cw < 2^len
+	{
+		acc = (acc << len) | cw;
+		nb += len;
+		// v_alignbit uses nb mod 32
+		atomicOr(img + __builtin_amdgcn_ubfe(nb, 5u, 27u) - 1,
+			 __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, nb));
+	}
+	__device__ __forceinline__ void flush()
+	{
+		if (nb & 31u)
+			atomicOr(img + (nb >> 5), (uint32_t)acc << (32u - (nb & 31u)));
+	}
+};
+
+// all-ones when q > 16 (q < 2^16)
+__device__ __forceinline__ uint32_t gt16_mask(uint32_t q)
+{
+	return (uint32_t)((int32_t)(16u - q) >> 31);
+}
+
 // ---------------------------------------------------------------------
 // the encode kernel
 //   W      bytes per input sample (2: u16/i16, 4: i16 in i32)
@@ -321,7 +403,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	constexpr uint32_t RW = W == 2 ? 2u : 4u; // uint4 per lane per chunk
 	constexpr bool EXT_HDR = !(PRE == PRE_NONE && ENC == ENC_RAW);
 	constexpr uint32_t HDR_BITS = EXT_HDR ? 176u : 128u;
-	__shared__ __attribute__((aligned(16))) uint32_t L[2][LWORDS];
+	__shared__ __attribute__((aligned(16))) uint32_t L[2][LWORDS + 4]; // [0..3]: guard
 	__shared__ uint32_t s_wsum[CH][AIRS_WG / 64];
 	__shared__ uint32_t s_misc[8];
 
@@ -385,7 +467,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// zero both LDS chunk images while the loads are in flight
 	{
 		uint4 *L4 = reinterpret_cast<uint4 *>(&L[0][0]);
-		for (uint32_t i = tid; i < 2u * LWORDS / 4u; i += AIRS_WG)
+		for (uint32_t i = tid; i < 2u * (LWORDS + 4u) / 4u; i += AIRS_WG)
 			L4[i] = make_uint4(0u, 0u, 0u, 0u);
 	}
 
@@ -393,6 +475,12 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	const Coder cd = make_coder<ENC>(ENC == ENC_RAW ? 1u : gpar, a.outlier_param);
 
 	// ---- phase 1: residuals, mapped values, code lengths ------------------
+	// Samples are handled as packed 16-bit pairs: DIFF is one v_pk_sub_u16
+	// against the pair shifted by one sample (v_alignbit), ZigZag three
+	// packed ops, and for Rice/ZERO with k <= 11 the code lengths are summed
+	// with packed ops too (length = k + 1 + min((m + 1) >> k, 16)).
+	const bool fastk = ENC == ENC_ZERO && RICE && cd.k <= 11u;
+	const uint32_t kmask = (1u << cd.k) - 1u;
 	uint32_t mp[CH][AIRS_PT / 2]; // mapped values, two 16-bit per register
 	uint32_t nmp[MODEL ? CH : 1][AIRS_PT / 2]; // new model values (MODEL)
 	uint32_t T[CH], nv[CH];
@@ -400,92 +488,105 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	for (uint32_t c = 0; c < CH; c++) {
 		const uint32_t first = firstc[c];
 		nv[c] = first >= n ? 0u : min(n - first, (uint32_t)AIRS_PT);
-		uint32_t x[AIRS_PT];
+		uint32_t w[AIRS_PT / 2]; // sample pairs (x[2j] | x[2j+1] << 16)
 		if (nv[c] == AIRS_PT && src_al) {
 			if (W == 2) {
 				const uint32_t w8[8] = {raw[c][0].x, raw[c][0].y, raw[c][0].z, raw[c][0].w,
 							raw[c][1].x, raw[c][1].y, raw[c][1].z, raw[c][1].w};
 #pragma unroll
-				for (int j = 0; j < 8; j++) {
-					x[2 * j] = w8[j] & 0xFFFFu;
-					x[2 * j + 1] = w8[j] >> 16;
-				}
+				for (int j = 0; j < 8; j++)
+					w[j] = w8[j];
 			} else {
 #pragma unroll
 				for (uint32_t q = 0; q < 4; q++) {
-					x[4 * q + 0] = raw[c][q].x & 0xFFFFu;
-					x[4 * q + 1] = raw[c][q].y & 0xFFFFu;
-					x[4 * q + 2] = raw[c][q].z & 0xFFFFu;
-					x[4 * q + 3] = raw[c][q].w & 0xFFFFu;
+					w[2 * q] = __builtin_amdgcn_perm(raw[c][q].y, raw[c][q].x, 0x05040100u);
+					w[2 * q + 1] = __builtin_amdgcn_perm(raw[c][q].w, raw[c][q].z, 0x05040100u);
 				}
 			}
 		} else {
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT; j++) {
-				const uint32_t i = first + j;
-				x[j] = i < n ? (W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fsrc)[i]
-						       : reinterpret_cast<const uint32_t *>(fsrc)[i] & 0xFFFFu)
-					     : 0u;
+			for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+				uint32_t x2[2];
+#pragma unroll
+				for (uint32_t h = 0; h < 2; h++) {
+					const uint32_t i = first + 2 * j + h;
+					x2[h] = i < n ? (W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fsrc)[i]
+								: reinterpret_cast<const uint32_t *>(fsrc)[i] & 0xFFFFu)
+						      : 0u;
+				}
+				w[j] = x2[0] | x2[1] << 16;
 			}
 		}
-		uint32_t mo[AIRS_PT];
+		uint32_t pm[AIRS_PT / 2]; // model pairs (MODEL == 2)
 		if (MODEL == 2) {
 			if (nv[c] == AIRS_PT && mod_al) {
 				const uint32_t w8[8] = {mraw[c][0].x, mraw[c][0].y, mraw[c][0].z, mraw[c][0].w,
 							mraw[c][1].x, mraw[c][1].y, mraw[c][1].z, mraw[c][1].w};
 #pragma unroll
-				for (int j = 0; j < 8; j++) {
-					mo[2 * j] = w8[j] & 0xFFFFu;
-					mo[2 * j + 1] = w8[j] >> 16;
-				}
+				for (int j = 0; j < 8; j++)
+					pm[j] = w8[j];
 			} else {
 #pragma unroll
-				for (uint32_t j = 0; j < AIRS_PT; j++)
-					mo[j] = first + j < n ? (uint32_t)reinterpret_cast<const uint16_t *>(fmodel)[first + j]
-							      : 0u;
+				for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+					uint32_t x2[2];
+#pragma unroll
+					for (uint32_t h = 0; h < 2; h++) {
+						const uint32_t i = first + 2 * j + h;
+						x2[h] = i < n ? (uint32_t)reinterpret_cast<const uint16_t *>(fmodel)[i] : 0u;
+					}
+					pm[j] = x2[0] | x2[1] << 16;
+				}
 			}
 		}
-		uint32_t prev = 0u;
+		uint32_t wprev = 0u; // pair whose high half is the sample before this lane's first
 		if (PRE == PRE_DIFF) {
-			prev = __shfl_up(x[AIRS_PT - 1], 1, 64);
+			wprev = __shfl_up(w[AIRS_PT / 2 - 1], 1, 64);
 			if (lane == 0u)
-				prev = prevld[c];
+				wprev = prevld[c] << 16;
 		}
-		uint32_t t = 0u;
 #pragma unroll
-		for (uint32_t j = 0; j < AIRS_PT; j++) {
+		for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
 			uint32_t u;
 			if (PRE == PRE_DIFF)
-				u = x[j] - (j ? x[j - 1] : prev);
+				u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
 			else if (PRE == PRE_MODEL)
-				u = x[j] - mo[j];
+				u = unpk(pk(w[j]) - pk(pm[j]));
 			else
-				u = x[j];
-			u &= 0xFFFFu;
-			const uint32_t m = ENC == ENC_RAW ? u : zigzag16(u);
-			const uint32_t l = j < nv[c] ? len_from_m<ENC, RICE>(m, cd) : 0u;
-			t += l;
-			if (j & 1u)
-				mp[c][j >> 1] |= m << 16;
-			else
-				mp[c][j >> 1] = m;
-			if (MODEL) {
-				uint32_t nm;
-				if (MODEL == 1) {
-					nm = x[j];
-				} else {
-					const int32_t rate = (int32_t)a.model_rate;
-					const int32_t d = a.is_unsigned ? (int32_t)x[j] : (int32_t)(int16_t)x[j];
-					const int32_t mm = a.is_unsigned ? (int32_t)mo[j] : (int32_t)(int16_t)mo[j];
-					nm = (uint32_t)((mm * rate + d * (16 - rate)) >> 4) & 0xFFFFu;
-				}
-				if (j & 1u)
-					nmp[MODEL ? c : 0][j >> 1] |= nm << 16;
-				else
-					nmp[MODEL ? c : 0][j >> 1] = nm;
-			}
+				u = w[j];
+			mp[c][j] = ENC == ENC_RAW ? u : zigzag_pk(u);
+		}
+		uint32_t t = 0u;
+		if (fastk && nv[c] == AIRS_PT) {
+			u16x2 acc = (u16x2)(0);
+#pragma unroll
+			for (uint32_t j = 0; j < AIRS_PT / 2; j++)
+				acc += pk(rice_pair(mp[c][j], cd.k, kmask).lq);
+			t = AIRS_PT * (cd.k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
+		} else {
+#pragma unroll
+			for (uint32_t j = 0; j < AIRS_PT; j++)
+				t += j < nv[c] ? len_from_m<ENC, RICE>(half16(mp[c][j >> 1], j & 1u), cd) : 0u;
 		}
 		T[c] = t;
+		if (MODEL) {
+#pragma unroll
+			for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+				if (MODEL == 1) {
+					nmp[MODEL ? c : 0][j] = w[j];
+				} else {
+					uint32_t nm2 = 0u;
+#pragma unroll
+					for (uint32_t h = 0; h < 2; h++) {
+						const uint32_t xv = half16(w[j], h), mv = half16(pm[j], h);
+						const int32_t rate = (int32_t)a.model_rate;
+						const int32_t d = a.is_unsigned ? (int32_t)xv : (int32_t)(int16_t)xv;
+						const int32_t mm = a.is_unsigned ? (int32_t)mv : (int32_t)(int16_t)mv;
+						nm2 |= ((uint32_t)((mm * rate + d * (16 - rate)) >> 4) & 0xFFFFu) << (16u * h);
+					}
+					nmp[MODEL ? c : 0][j] = nm2;
+				}
+			}
+		}
 		// Make the packed mapped values opaque: otherwise the compiler keeps
 		// phase 1's per-sample intermediates alive to CSE them with phase 2's
 		// recomputation, which costs ~100 extra VGPRs and halves occupancy.
@@ -572,7 +673,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	uint32_t tot_m1 = 0u;
 #pragma unroll 1
 	for (uint32_t c = 0; c < CH; c++) {
-		uint32_t *Lc = L[c & 1u];
+		uint32_t *Lc = &L[c & 1u][4];
 		if (c >= 2) {
 			// image c&1 was last read by chunk c-2's stores (before the barrier
 			// that ended chunk c-1's packing): clear what it used
@@ -581,38 +682,48 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				Lc[i] = 0u;
 			__syncthreads();
 		}
-		uint32_t cw[NPIECE][AIRS_PT], ln[NPIECE][AIRS_PT];
-#pragma unroll
-		for (uint32_t j = 0; j < AIRS_PT; j++) {
-			const uint32_t m = (mp[0][j >> 1] >> (16u * (j & 1u))) & 0xFFFFu;
-			uint32_t c1, l1, c2, l2;
-			code_from_m<ENC, RICE>(m, cd, c1, l1, c2, l2);
-			const bool ok = j < nv[0];
-			cw[0][j] = ok ? c1 : 0u;
-			ln[0][j] = ok ? l1 : 0u;
-			if (NPIECE == 2) {
-				cw[NPIECE - 1][j] = ok ? c2 : 0u;
-				ln[NPIECE - 1][j] = ok ? l2 : 0u;
-			}
-		}
+		uint32_t ln[NPIECE][AIRS_PT]; // piece lengths (kept for the MODEL fail_bit check)
 		{
-			uint32_t wpos = excl[0] >> 5, nb = excl[0] & 31u;
-			uint64_t acc = 0u;
+			Packer pk1;
+			pk1.init(Lc, excl[0]);
+			if (fastk && nv[0] == AIRS_PT) {
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT; j++) {
+				for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+					const RicePair rp = rice_pair(mp[0][j], cd.k, kmask);
 #pragma unroll
-				for (uint32_t p = 0; p < NPIECE; p++) {
-					acc = (acc << ln[p][j]) | cw[p][j];
-					nb += ln[p][j];
-					const bool e = nb >= 32u;
-					nb -= e ? 32u : 0u;
-					// branch-free: OR 0 into the current word when nothing completed
-					atomicOr(&Lc[wpos], e ? (uint32_t)(acc >> nb) : 0u);
-					wpos += e ? 1u : 0u;
+					for (uint32_t h = 0; h < 2; h++) {
+						const uint32_t q = half16(rp.q, h), lq = half16(rp.lq, h);
+						const uint32_t len = cd.k + 1u + lq;
+						// q > 16: zero-escape, codeword 0 (k+1 bits) then the 16-bit
+						// value; otherwise q = lq ones, a zero and k low bits.
+						// Blended, not selected: a select here becomes a branch.
+						const uint32_t e = gt16_mask(q);
+						const uint32_t ne = bfm32(lq, cd.k + 1u) | half16(rp.low, h);
+						const uint32_t cw = (e & half16(mp[0][j], h)) | (~e & ne);
+						pk1.put(cw, len);
+						ln[0][2 * j + h] = len;
+						if (NPIECE == 2)
+							ln[NPIECE - 1][2 * j + h] = 0u;
+					}
+				}
+			} else {
+#pragma unroll
+				for (uint32_t j = 0; j < AIRS_PT; j++) {
+					const uint32_t m = half16(mp[0][j >> 1], j & 1u);
+					uint32_t c1, l1, c2, l2;
+					code_from_m<ENC, RICE>(m, cd, c1, l1, c2, l2);
+					const bool ok = j < nv[0];
+					l1 = ok ? l1 : 0u;
+					pk1.put(ok ? c1 : 0u, l1);
+					ln[0][j] = l1;
+					if (NPIECE == 2) {
+						l2 = ok ? l2 : 0u;
+						pk1.put(ok ? c2 : 0u, l2);
+						ln[NPIECE - 1][j] = l2;
+					}
 				}
 			}
-			if (nb)
-				atomicOr(&Lc[wpos], (uint32_t)(acc << (32u - nb)));
+			pk1.flush();
 		}
 		__syncthreads();
 		uint32_t pred_next = 0u; // last 32 bits of this chunk, for chunk c+1 (tid 0)
