@@ -407,7 +407,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	__shared__ uint32_t s_wsum[CH][AIRS_WG / 64];
 	__shared__ uint32_t s_misc[8];
 
-	const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+	const uint32_t tid = threadIdx.x, lane = tid & 63u;
+	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform
 
 	// ---- segment id: dispatch order (or an atomic ticket, debug switch) ----
 	uint32_t seg = blockIdx.x;
@@ -415,7 +416,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		if (tid == 0)
 			s_misc[0] = atomicAdd(a.ticket, 1u) - a.ticket_base;
 		__syncthreads();
-		seg = s_misc[0];
+		seg = __builtin_amdgcn_readfirstlane(s_misc[0]);
 	}
 	// Frame-interleaved dispatch: consecutive blocks take the same segment
 	// index of consecutive frames.  A frame's segments are still dispatched in
@@ -425,7 +426,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	const uint32_t sif = seg / nfr;
 	const uint32_t lf = seg - sif * nfr;
 	const uint32_t gseg = lf * a.segs_per_frame + sif; // granule slot: frame-major
-	const uint32_t frame = a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul;
+	const uint32_t frame =
+		__builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
 	const bool is_first = sif == 0u;
 	const bool is_last = sif + 1u == a.segs_per_frame;
 	const uint32_t n = a.n;
@@ -471,7 +473,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			L4[i] = make_uint4(0u, 0u, 0u, 0u);
 	}
 
-	const uint32_t gpar = a.frame_g ? a.frame_g[frame] : a.g;
+	const uint32_t gpar = __builtin_amdgcn_readfirstlane(a.frame_g ? a.frame_g[frame] : a.g);
 	const Coder cd = make_coder<ENC>(ENC == ENC_RAW ? 1u : gpar, a.outlier_param);
 
 	// ---- phase 1: residuals, mapped values, code lengths ------------------
@@ -556,7 +558,9 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			mp[c][j] = ENC == ENC_RAW ? u : zigzag_pk(u);
 		}
 		uint32_t t = 0u;
-		if (fastk && nv[c] == AIRS_PT) {
+		if (a.dbg & 64u) {
+			t = AIRS_PT * (cd.k + 1u) + (mp[c][0] & 7u);
+		} else if (fastk && nv[c] == AIRS_PT) {
 			u16x2 acc = (u16x2)(0);
 #pragma unroll
 			for (uint32_t j = 0; j < AIRS_PT / 2; j++)
@@ -619,7 +623,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			tt += v;
 		}
 		excl[c] = woff + inc[c] - T[c];
-		tot[c] = tt;
+		tot[c] = __builtin_amdgcn_readfirstlane(tt); // LDS-loaded, but block-uniform
 		base[c] = A;
 		A += tt;
 	}
@@ -635,7 +639,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				gv0 = gran_load(&a.agg[idx]);
 		}
 	}
-	if (!is_last && wid == AIRS_WG / 64 - 1) {
+	if (!is_last && wid == AIRS_WG / 64 - 1 && !(a.dbg & 8u)) {
 		// lane 255 holds >= 16 bits of the last chunk; lane 254 supplies the rest
 		uint64_t acc = 0u;
 #pragma unroll
@@ -663,6 +667,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 
 	uint8_t *fdst = a.dst + (uint64_t)frame * a.dst_stride;
 	const uint32_t cap = a.cap;
+	const __amdgpu_buffer_rsrc_t dst_rsrc = __builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(cap & ~3u), 0x00020000);
 	uint32_t P = 0u;
 	uint32_t pred_c = 0u; // (lane 0 of wave 0) bits preceding chunk c in its first dword
 
@@ -686,7 +691,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		{
 			Packer pk1;
 			pk1.init(Lc, excl[0]);
-			if (fastk && nv[0] == AIRS_PT) {
+			if (a.dbg & 32u) {
+			} else if (fastk && nv[0] == AIRS_PT) {
 #pragma unroll
 				for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
 					const RicePair rp = rice_pair(mp[0][j], cd.k, kmask);
@@ -827,36 +833,34 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				}
 			}
 			__syncthreads();
-			P = s_misc[1];
-			pred_c = s_misc[2];
+			P = __builtin_amdgcn_readfirstlane(s_misc[1]);
+			pred_c = __builtin_amdgcn_readfirstlane(s_misc[2]);
 		}
 
 		// ---- store chunk c: funnel-shift the image to its frame bit offset ----
+		// complete words go out through a buffer descriptor whose range is the
+		// frame's capacity rounded down to whole words, so the hardware range
+		// check drops exactly the words that would not fit
 		if (tot[0]) {
 			const uint32_t Pc = P + base[0];
 			const uint32_t r = Pc & 31u, g0 = Pc >> 5;
 			const uint32_t endbit = Pc + tot[0];
-			const uint32_t J = ((endbit - 1u) >> 5) - g0;
-			const bool last_complete = (endbit & 31u) == 0u;
-			const bool final_chunk = is_last && c == last_ne;
-			for (uint32_t j = tid; j <= J; j += AIRS_WG) {
-				uint32_t hi;
-				if (j)
-					hi = Lc[j - 1u];
-				else
-					hi = pred_c;
+			const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
+			const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
+			for (uint32_t j = tid; j < nfull; j += AIRS_WG) {
+				const uint32_t hi = j ? Lc[j - 1u] : pred_c;
 				const uint32_t v = __builtin_amdgcn_alignbit(hi, Lc[j], r);
-				const uint32_t gw = g0 + j;
-				if (j < J || last_complete) {
-					if (4u * gw + 4u <= cap)
-						*reinterpret_cast<uint32_t *>(fdst + 4u * gw) = bswap32(v);
-				} else if (final_chunk) {
-					// zero-padded final bytes of the payload (reference bitstream_flush)
-					const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
-					for (uint32_t b = 0; b < nbytes; b++)
-						if (4u * gw + b < cap)
-							fdst[4u * gw + b] = (uint8_t)(v >> (24u - 8u * b));
-				}
+				__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
+			}
+			if (is_last && c == last_ne && nfull == J && tid == 0) {
+				// zero-padded final bytes of the payload (reference bitstream_flush)
+				const uint32_t hi = J ? Lc[J - 1u] : pred_c;
+				const uint32_t v = __builtin_amdgcn_alignbit(hi, Lc[J], r);
+				const uint32_t gw = g0 + J;
+				const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
+				for (uint32_t b = 0; b < nbytes; b++)
+					if (4u * gw + b < cap)
+						fdst[4u * gw + b] = (uint8_t)(v >> (24u - 8u * b));
 			}
 		}
 
