@@ -44,7 +44,8 @@ def _one_hip_runtime() -> None:
 
 
 def load(path: str | None = None) -> "AirsLib":
-    path = path or LIB_PATH
+    # AIRS_LIB: developer override (benchmarking an alternative build)
+    path = path or os.environ.get("AIRS_LIB") or LIB_PATH
     _one_hip_runtime()
     if not os.path.exists(path):
         raise FileNotFoundError(

@@ -343,6 +343,9 @@ struct Packer {
 	uint64_t acc;
 	uint32_t nb;
 	uint32_t *img;
+#if defined(AIRS_EXP_SINK)
+	uint32_t sink = 0u;
+#endif
 
 	__device__ __forceinline__ void init(uint32_t *image, uint32_t bit)
 	{
@@ -355,15 +358,37 @@ struct Packer {
 		acc = (acc << len) | cw;
 		nb += len;
 		// v_alignbit uses nb mod 32
+#if defined(AIRS_EXP_SINK)
+		sink ^= __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, nb) + (uint32_t)(uintptr_t)(img + __builtin_amdgcn_ubfe(nb, 5u, 27u) - 1);
+#elif defined(AIRS_EXP_WRITE)
+		img[__builtin_amdgcn_ubfe(nb, 5u, 27u) - 1] = __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, nb);
+#else
 		atomicOr(img + __builtin_amdgcn_ubfe(nb, 5u, 27u) - 1,
 			 __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, nb));
+#endif
 	}
 	__device__ __forceinline__ void flush()
 	{
+#if defined(AIRS_EXP_SINK)
+		atomicOr(img + (nb >> 5), sink);
+#endif
 		if (nb & 31u)
 			atomicOr(img + (nb >> 5), (uint32_t)acc << (32u - (nb & 31u)));
 	}
 };
+
+// Rice/ZERO codeword table.  With v = m + 1 = q*2^k + low and q <= 16 the
+// codeword is ((2^q - 1) << (k+1)) | low = v + 2^(q+k+1) - 2^(k+1) - q*2^k, so
+// codeword = m + T'[q] with T'[q] = 2^(q+k+1) - 2^(k+1) - q*2^k + 1; every
+// q >= 17 is the zero-escape, codeword m (T'[17] = 0), length k+17.
+// Valid for k <= 11 (codewords < 2^29).
+__device__ __forceinline__ uint2 rice_table_entry(uint32_t q, uint32_t k)
+{
+	if (q >= 17u)
+		return make_uint2(0u, k + 17u);
+	const uint32_t t = (1u << (q + k + 1u)) - (2u << k) - (q << k) + 1u;
+	return make_uint2(t, k + 1u + q);
+}
 
 // all-ones when q > 16 (q < 2^16)
 __device__ __forceinline__ uint32_t gt16_mask(uint32_t q)
@@ -406,6 +431,9 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	__shared__ __attribute__((aligned(16))) uint32_t L[2][LWORDS + 4]; // [0..3]: guard
 	__shared__ uint32_t s_wsum[CH][AIRS_WG / 64];
 	__shared__ uint32_t s_misc[8];
+	// Rice/ZERO code table (fast path): entry q' = min(q, 17) holds
+	// {T'[q'], len[q']} with codeword = m + T'[q'] (see rice_table)
+	__shared__ __attribute__((aligned(16))) uint2 s_rice[20];
 
 	const uint32_t tid = threadIdx.x, lane = tid & 63u;
 	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform
@@ -483,6 +511,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// with packed ops too (length = k + 1 + min((m + 1) >> k, 16)).
 	const bool fastk = ENC == ENC_ZERO && RICE && cd.k <= 11u;
 	const uint32_t kmask = (1u << cd.k) - 1u;
+	if (fastk && tid < 18u)
+		s_rice[tid] = rice_table_entry(tid, cd.k);
 	uint32_t mp[CH][AIRS_PT / 2]; // mapped values, two 16-bit per register
 	uint32_t nmp[MODEL ? CH : 1][AIRS_PT / 2]; // new model values (MODEL)
 	uint32_t T[CH], nv[CH];
@@ -693,24 +723,27 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			pk1.init(Lc, excl[0]);
 			if (a.dbg & 32u) {
 			} else if (fastk && nv[0] == AIRS_PT) {
+				// table-driven: byte offsets 8*min(q, 17) of both samples of a
+				// pair come from three packed ops; codeword = m + T'[q']
+				// (all 16 lookups are issued before the first put: the compiler
+				// does not move LDS reads across the packer's ds_or atomics)
+				const char *tab = reinterpret_cast<const char *>(s_rice);
+				uint2 te[AIRS_PT];
 #pragma unroll
 				for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
-					const RicePair rp = rice_pair(mp[0][j], cd.k, kmask);
+					const u16x2 v = __builtin_elementwise_add_sat(pk(mp[0][j]), (u16x2)(1));
+					const u16x2 qa = __builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17))
+							 << (u16x2)(3);
 #pragma unroll
-					for (uint32_t h = 0; h < 2; h++) {
-						const uint32_t q = half16(rp.q, h), lq = half16(rp.lq, h);
-						const uint32_t len = cd.k + 1u + lq;
-						// q > 16: zero-escape, codeword 0 (k+1 bits) then the 16-bit
-						// value; otherwise q = lq ones, a zero and k low bits.
-						// Blended, not selected: a select here becomes a branch.
-						const uint32_t e = gt16_mask(q);
-						const uint32_t ne = bfm32(lq, cd.k + 1u) | half16(rp.low, h);
-						const uint32_t cw = (e & half16(mp[0][j], h)) | (~e & ne);
-						pk1.put(cw, len);
-						ln[0][2 * j + h] = len;
-						if (NPIECE == 2)
-							ln[NPIECE - 1][2 * j + h] = 0u;
-					}
+					for (uint32_t h = 0; h < 2; h++)
+						te[2 * j + h] = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
+				}
+#pragma unroll
+				for (uint32_t j = 0; j < AIRS_PT; j++) {
+					pk1.put(half16(mp[0][j >> 1], j & 1u) + te[j].x, te[j].y);
+					ln[0][j] = te[j].y;
+					if (NPIECE == 2)
+						ln[NPIECE - 1][j] = 0u;
 				}
 			} else {
 #pragma unroll
