@@ -39,7 +39,9 @@
 
 #include "airs_dev.h"
 
+#ifndef AIRS_WG
 #define AIRS_WG 256
+#endif
 #define AIRS_PT 16
 #define AIRS_SEG (AIRS_WG * AIRS_PT)
 // bounded spins: ~2^22 polls with s_sleep is far beyond any legitimate wait
@@ -639,7 +641,11 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	}
 
 	// ---- the segment's last 32 bits (wave 3 rebuilds its last chunk) ------
-	uint64_t gv0 = 0;
+	constexpr int LB_WIN = 4; // look-back windows of 64 granules fetched per round
+	uint64_t gv[LB_WIN];
+#pragma unroll
+	for (int w = 0; w < LB_WIN; w++)
+		gv[w] = 0;
 	__syncthreads(); // B1: wave totals visible
 	uint32_t excl[CH], tot[CH], base[CH];
 	uint32_t A = 0u;
@@ -658,15 +664,23 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		A += tt;
 	}
 	const uint32_t first_seg = gseg - sif;
+	uint64_t tv0 = 0; // predecessor's tail granule, fetched early (lane 0 of wave 0)
 	if (wid == 0) {
 		if (lane == 0) {
 			const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
 			gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
 		}
 		if (!is_first && !(a.dbg & 2u)) {
-			const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane;
-			if (idx >= (int64_t)first_seg)
-				gv0 = gran_load(&a.agg[idx]);
+			// the first round's windows, newest first: with ~64 segments of a
+			// frame in flight the nearest inclusive prefix is often past 64
+#pragma unroll
+			for (int w = 0; w < LB_WIN; w++) {
+				const int64_t idx = (int64_t)gseg - 1 - 64 * w - (int64_t)lane;
+				if (idx >= (int64_t)first_seg)
+					gv[w] = gran_load(&a.agg[idx]);
+			}
+			if (lane == 0)
+				tv0 = gran_load(&a.tail[gseg - 1u]);
 		}
 	}
 	if (!is_last && wid == AIRS_WG / 64 - 1 && !(a.dbg & 8u)) {
@@ -778,19 +792,14 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				if (a.dbg & 2u) {
 					Pw = HDR_BITS + sif * 37u; // ablation: no look-back (output garbage)
 				} else if (!is_first) {
-					// round 0 uses the 64 granules fetched before packing; later
-					// rounds fetch LB_WIN windows of 64 at once, newest first
-					constexpr int LB_WIN = 4;
-					uint32_t sum = 0u, spins = 0u;
+					// round 0 uses the granules fetched before packing; every
+					// round covers LB_WIN windows of 64, newest first
+					uint32_t sum = 0u, spins = 0u, lb_rounds = 0u;
 					int64_t j = (int64_t)gseg - 1;
-					uint64_t gv[LB_WIN];
-					int nwin = 1;
-					gv[0] = gv0;
-#pragma unroll
-					for (int w = 1; w < LB_WIN; w++)
-						gv[w] = 0;
+					int nwin = LB_WIN;
 					bool done = false;
 					while (!done) {
+						lb_rounds++;
 						bool retry = false;
 #pragma unroll
 						for (int w = 0; w < LB_WIN; w++) {
@@ -840,6 +849,11 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 					Pw = sum;
 					if (lane == 0)
 						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (Pw + A));
+					if ((a.dbg & 256u) && lane == 0) { // look-back statistics (debug)
+						atomicAdd(a.ticket + 20, 1u);
+						atomicAdd(a.ticket + 21, lb_rounds);
+						atomicAdd(a.ticket + 22, spins);
+					}
 				}
 				if (lane == 0) {
 					uint32_t pred = 0u;
@@ -848,16 +862,16 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 						// the first payload dword of a 22-byte header
 						pred = (EXT_HDR && ENC != ENC_RAW) ? (cd.outlier & 0xFFFFu) : 0u;
 					} else {
-						uint64_t tv;
-						for (uint32_t spins = 0;; spins++) {
-							tv = gran_load(&a.tail[gseg - 1u]);
-							if ((uint32_t)(tv >> 32) == a.epoch)
-								break;
+						uint64_t tv = tv0;
+						for (uint32_t spins = 0; (uint32_t)(tv >> 32) != a.epoch; spins++) {
 							if (spins > AIRS_SPIN_LIMIT) {
 								atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
 								break;
 							}
 							__builtin_amdgcn_s_sleep(1);
+							tv = gran_load(&a.tail[gseg - 1u]);
+							if (a.dbg & 256u)
+								atomicAdd(a.ticket + 23, 1u);
 						}
 						pred = (uint32_t)tv;
 					}
@@ -1539,6 +1553,20 @@ extern "C" uint32_t airs_dev_sync(struct airs_dev_engine *e)
 	uint32_t faults = 0;
 	HIPCHECK(hipStreamSynchronize(e->stream));
 	HIPCHECK(hipMemcpy(&faults, e->ticket + AIRS_FAULT_WORD, sizeof(faults), hipMemcpyDeviceToHost));
+	{
+		static int dbg = -1;
+		if (dbg < 0) {
+			const char *v = getenv("AIRS_DBG");
+			dbg = v ? atoi(v) : 0;
+		}
+		if (dbg & 256) {
+			uint32_t st[4];
+			HIPCHECK(hipMemcpy(st, e->ticket + 20, sizeof(st), hipMemcpyDeviceToHost));
+			fprintf(stderr, "airscmp look-back stats: lookbacks=%u rounds=%u retries=%u tail_repolls=%u\n", st[0],
+				st[1], st[2], st[3]);
+			(void)hipMemset(e->ticket + 20, 0, sizeof(st));
+		}
+	}
 	if (faults) {
 		snprintf(g_err, sizeof(g_err), "%u look-back give-ups", faults);
 		fprintf(stderr, "airscmp: internal error: %s\n", g_err);

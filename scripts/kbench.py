@@ -39,6 +39,7 @@ for k in range(40):
     if k >= 10:
         ev[k - 10][1].record(stream)
 torch.cuda.synchronize()
+eng.synchronize()
 ms = sorted(a.elapsed_time(b) for a, b in ev)
 print(json.dumps(dict(workload=sys.argv[1], dbg=os.environ.get("AIRS_DBG", "0"), median_ms=ms[len(ms) // 2],
                       min_ms=ms[0], GBps=round(nf * 2 * n / (ms[len(ms) // 2] * 1e-3) / 1e9, 1))))
