@@ -427,6 +427,15 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	constexpr uint32_t MAXBITS = ENC == ENC_RAW ? 16u : (ENC == ENC_ZERO ? 32u : 48u);
 	constexpr uint32_t LWORDS = AIRS_SEG * MAXBITS / 32u + 4u; // one chunk image
 	constexpr uint32_t NPIECE = ENC == ENC_MULTI ? 2 : 1;
+	// Chunk after whose packing the look-back is evaluated.  1: wave 0 issues
+	// the granule loads when chunk 1's packing starts and reads them when it
+	// ends, so they see the predecessors one chunk later than the aggregate
+	// publish (which an earlier poll mostly misses); chunk 0 is stored late.
+	// 0 with a model, whose chunk-0 update needs the bit offset first.
+#ifndef AIRS_LBC
+#define AIRS_LBC 1u
+#endif
+	constexpr uint32_t LBC = (MODEL || CH < 2) ? 0u : AIRS_LBC;
 	constexpr uint32_t RW = W == 2 ? 2u : 4u; // uint4 per lane per chunk
 	constexpr bool EXT_HDR = !(PRE == PRE_NONE && ENC == ENC_RAW);
 	constexpr uint32_t HDR_BITS = EXT_HDR ? 176u : 128u;
@@ -670,7 +679,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
 			gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
 		}
-		if (!is_first && !(a.dbg & 2u)) {
+		if (LBC == 0 && !is_first && !(a.dbg & 2u)) {
 			// the first round's windows, newest first: with ~64 segments of a
 			// frame in flight the nearest inclusive prefix is often past 64
 #pragma unroll
@@ -714,6 +723,36 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	const __amdgpu_buffer_rsrc_t dst_rsrc = __builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(cap & ~3u), 0x00020000);
 	uint32_t P = 0u;
 	uint32_t pred_c = 0u; // (lane 0 of wave 0) bits preceding chunk c in its first dword
+	const uint32_t tot_first = tot[0];
+
+	// Store one chunk image: funnel-shift it to its frame bit offset.  Complete
+	// words go out through a buffer descriptor whose range is the frame's
+	// capacity rounded down to whole words, so the hardware range check drops
+	// exactly the words that would not fit.
+	auto store_chunk = [&](const uint32_t *Lx, uint32_t basex, uint32_t totx, uint32_t predx, bool finalx) {
+		if (!totx)
+			return;
+		const uint32_t Pc = P + basex;
+		const uint32_t r = Pc & 31u, g0 = Pc >> 5;
+		const uint32_t endbit = Pc + totx;
+		const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
+		const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
+		for (uint32_t j = tid; j < nfull; j += AIRS_WG) {
+			const uint32_t hi = j ? Lx[j - 1u] : predx;
+			const uint32_t v = __builtin_amdgcn_alignbit(hi, Lx[j], r);
+			__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
+		}
+		if (finalx && nfull == J && tid == 0) {
+			// zero-padded final bytes of the payload (reference bitstream_flush)
+			const uint32_t hi = J ? Lx[J - 1u] : predx;
+			const uint32_t v = __builtin_amdgcn_alignbit(hi, Lx[J], r);
+			const uint32_t gw = g0 + J;
+			const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
+			for (uint32_t b = 0; b < nbytes; b++)
+				if (4u * gw + b < cap)
+					fdst[4u * gw + b] = (uint8_t)(v >> (24u - 8u * b));
+		}
+	};
 
 	// ---- phase 2: chunk by chunk: codewords -> LDS image -> HBM -----------
 	// rolled loop (keeps register pressure flat): the current chunk's state is
@@ -723,6 +762,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 #pragma unroll 1
 	for (uint32_t c = 0; c < CH; c++) {
 		uint32_t *Lc = &L[c & 1u][4];
+		if (LBC == 1 && c == 2u)
+			__syncthreads(); // chunk 0's image was stored (late) after the last barrier
 		if (c >= 2) {
 			// image c&1 was last read by chunk c-2's stores (before the barrier
 			// that ended chunk c-1's packing): clear what it used
@@ -730,6 +771,16 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			for (uint32_t i = tid; i <= nw; i += AIRS_WG)
 				Lc[i] = 0u;
 			__syncthreads();
+		}
+		if (LBC == 1 && c == 1u && wid == 0 && !is_first && !(a.dbg & 2u)) {
+#pragma unroll
+			for (int w = 0; w < LB_WIN; w++) {
+				const int64_t idx = (int64_t)gseg - 1 - 64 * w - (int64_t)lane;
+				if (idx >= (int64_t)first_seg)
+					gv[w] = gran_load(&a.agg[idx]);
+			}
+			if (lane == 0)
+				tv0 = gran_load(&a.tail[gseg - 1u]);
 		}
 		uint32_t ln[NPIECE][AIRS_PT]; // piece lengths (kept for the MODEL fail_bit check)
 		{
@@ -785,7 +836,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			pred_next = sh ? (Lc[q] << sh) | (Lc[q + 1] >> (32u - sh)) : Lc[q];
 		}
 
-		if (c == 0) {
+		if (c == LBC) {
 			// ---- decoupled look-back (wave 0), overlapped with the packing ----
 			if (wid == 0) {
 				uint32_t Pw = HDR_BITS;
@@ -881,35 +932,15 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			}
 			__syncthreads();
 			P = __builtin_amdgcn_readfirstlane(s_misc[1]);
-			pred_c = __builtin_amdgcn_readfirstlane(s_misc[2]);
+			const uint32_t seg_pred = __builtin_amdgcn_readfirstlane(s_misc[2]);
+			if (LBC == 0)
+				pred_c = seg_pred;
+			else if (tot_first) // chunk 0 waited for the look-back: store it now
+				store_chunk(&L[0][4], 0u, tot_first, seg_pred, is_last && last_ne == 0u);
 		}
 
-		// ---- store chunk c: funnel-shift the image to its frame bit offset ----
-		// complete words go out through a buffer descriptor whose range is the
-		// frame's capacity rounded down to whole words, so the hardware range
-		// check drops exactly the words that would not fit
-		if (tot[0]) {
-			const uint32_t Pc = P + base[0];
-			const uint32_t r = Pc & 31u, g0 = Pc >> 5;
-			const uint32_t endbit = Pc + tot[0];
-			const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
-			const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
-			for (uint32_t j = tid; j < nfull; j += AIRS_WG) {
-				const uint32_t hi = j ? Lc[j - 1u] : pred_c;
-				const uint32_t v = __builtin_amdgcn_alignbit(hi, Lc[j], r);
-				__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
-			}
-			if (is_last && c == last_ne && nfull == J && tid == 0) {
-				// zero-padded final bytes of the payload (reference bitstream_flush)
-				const uint32_t hi = J ? Lc[J - 1u] : pred_c;
-				const uint32_t v = __builtin_amdgcn_alignbit(hi, Lc[J], r);
-				const uint32_t gw = g0 + J;
-				const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
-				for (uint32_t b = 0; b < nbytes; b++)
-					if (4u * gw + b < cap)
-						fdst[4u * gw + b] = (uint8_t)(v >> (24u - 8u * b));
-			}
-		}
+		if (c >= LBC)
+			store_chunk(Lc, base[0], tot[0], pred_c, is_last && c == last_ne);
 
 		// ---- model update of chunk c (cmp.c:304-311), old model kept for the
 		// samples the reference's loop never reached (see fail_bit) ----------
