@@ -695,14 +695,29 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	if (!is_last && wid == AIRS_WG / 64 - 1 && !(a.dbg & 8u)) {
 		// lane 255 holds >= 16 bits of the last chunk; lane 254 supplies the rest
 		uint64_t acc = 0u;
+		if (fastk && nv[CH - 1] == AIRS_PT) {
+			const char *tab = reinterpret_cast<const char *>(s_rice);
 #pragma unroll
-		for (uint32_t j = 0; j < AIRS_PT; j++) {
-			const uint32_t m = (mp[CH - 1][j >> 1] >> (16u * (j & 1u))) & 0xFFFFu;
-			uint32_t c1, l1, c2, l2;
-			code_from_m<ENC, RICE>(m, cd, c1, l1, c2, l2);
-			acc = (acc << l1) | c1;
-			if (NPIECE == 2)
-				acc = (acc << l2) | c2;
+			for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+				const u16x2 v = __builtin_elementwise_add_sat(pk(mp[CH - 1][j]), (u16x2)(1));
+				const u16x2 qa = __builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17))
+						 << (u16x2)(3);
+#pragma unroll
+				for (uint32_t h = 0; h < 2; h++) {
+					const uint2 e = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
+					acc = (acc << e.y) | (half16(mp[CH - 1][j], h) + e.x);
+				}
+			}
+		} else {
+#pragma unroll
+			for (uint32_t j = 0; j < AIRS_PT; j++) {
+				const uint32_t m = (mp[CH - 1][j >> 1] >> (16u * (j & 1u))) & 0xFFFFu;
+				uint32_t c1, l1, c2, l2;
+				code_from_m<ENC, RICE>(m, cd, c1, l1, c2, l2);
+				acc = (acc << l1) | c1;
+				if (NPIECE == 2)
+					acc = (acc << l2) | c2;
+			}
 		}
 		const uint32_t lo = (uint32_t)acc;
 		const uint32_t lo_prev = __shfl_up(lo, 1, 64);
@@ -793,22 +808,28 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				// (all 16 lookups are issued before the first put: the compiler
 				// does not move LDS reads across the packer's ds_or atomics)
 				const char *tab = reinterpret_cast<const char *>(s_rice);
-				uint2 te[AIRS_PT];
 #pragma unroll
-				for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
-					const u16x2 v = __builtin_elementwise_add_sat(pk(mp[0][j]), (u16x2)(1));
-					const u16x2 qa = __builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17))
-							 << (u16x2)(3);
+				for (uint32_t hb = 0; hb < 2; hb++) { // two batches of 8 lookups
+					uint2 te[AIRS_PT / 2];
 #pragma unroll
-					for (uint32_t h = 0; h < 2; h++)
-						te[2 * j + h] = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
-				}
+					for (uint32_t jj = 0; jj < AIRS_PT / 4; jj++) {
+						const uint32_t j = hb * (AIRS_PT / 4) + jj;
+						const u16x2 v = __builtin_elementwise_add_sat(pk(mp[0][j]), (u16x2)(1));
+						const u16x2 qa =
+							__builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17))
+							<< (u16x2)(3);
 #pragma unroll
-				for (uint32_t j = 0; j < AIRS_PT; j++) {
-					pk1.put(half16(mp[0][j >> 1], j & 1u) + te[j].x, te[j].y);
-					ln[0][j] = te[j].y;
-					if (NPIECE == 2)
-						ln[NPIECE - 1][j] = 0u;
+						for (uint32_t h = 0; h < 2; h++)
+							te[2 * jj + h] = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
+					}
+#pragma unroll
+					for (uint32_t i = 0; i < AIRS_PT / 2; i++) {
+						const uint32_t j = hb * (AIRS_PT / 2) + i;
+						pk1.put(half16(mp[0][j >> 1], j & 1u) + te[i].x, te[i].y);
+						ln[0][j] = te[i].y;
+						if (NPIECE == 2)
+							ln[NPIECE - 1][j] = 0u;
+					}
 				}
 			} else {
 #pragma unroll
