@@ -82,6 +82,7 @@ struct KArgs {
 	uint32_t model_mode, model_rate, is_unsigned, checksum;
 	uint32_t seq, pre_hdr, enc_hdr, model_rate_hdr;
 	uint32_t ticket_base, epoch;
+	uint32_t img_words; // LDS image size: AIRS_SEG * (longest codeword) / 32 + 4, multiple of 4
 	uint32_t dbg; // ablation switches (AIRS_DBG env, benchmarking only; 0 in production)
 };
 
@@ -424,8 +425,6 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 {
 	constexpr uint32_t CH = seg_chunks(W, MODEL);
 	constexpr uint32_t SEGN = CH * AIRS_SEG;
-	constexpr uint32_t MAXBITS = ENC == ENC_RAW ? 16u : (ENC == ENC_ZERO ? 32u : 48u);
-	constexpr uint32_t LWORDS = AIRS_SEG * MAXBITS / 32u + 4u; // one chunk image
 	constexpr uint32_t NPIECE = ENC == ENC_MULTI ? 2 : 1;
 	// Chunk after whose packing the look-back is evaluated.  1: wave 0 issues
 	// the granule loads when chunk 1's packing starts and reads them when it
@@ -439,7 +438,10 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	constexpr uint32_t RW = W == 2 ? 2u : 4u; // uint4 per lane per chunk
 	constexpr bool EXT_HDR = !(PRE == PRE_NONE && ENC == ENC_RAW);
 	constexpr uint32_t HDR_BITS = EXT_HDR ? 176u : 128u;
-	__shared__ __attribute__((aligned(16))) uint32_t L[2][LWORDS + 4]; // [0..3]: guard
+	// two chunk images in dynamic LDS, a.img_words each (sized per launch from
+	// the longest codeword the pass can emit), each after a 4-word guard
+	extern __shared__ __attribute__((aligned(16))) uint32_t L_dyn[];
+	const uint32_t IMGW = a.img_words + 4u; // words per image incl. guard (multiple of 4)
 	__shared__ uint32_t s_wsum[CH][AIRS_WG / 64];
 	__shared__ uint32_t s_misc[8];
 	// Rice/ZERO code table (fast path): entry q' = min(q, 17) holds
@@ -507,8 +509,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 
 	// zero both LDS chunk images while the loads are in flight
 	{
-		uint4 *L4 = reinterpret_cast<uint4 *>(&L[0][0]);
-		for (uint32_t i = tid; i < 2u * (LWORDS + 4u) / 4u; i += AIRS_WG)
+		uint4 *L4 = reinterpret_cast<uint4 *>(L_dyn);
+		for (uint32_t i = tid; i < 2u * IMGW / 4u; i += AIRS_WG)
 			L4[i] = make_uint4(0u, 0u, 0u, 0u);
 	}
 
@@ -776,7 +778,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	uint32_t tot_m1 = 0u;
 #pragma unroll 1
 	for (uint32_t c = 0; c < CH; c++) {
-		uint32_t *Lc = &L[c & 1u][4];
+		uint32_t *Lc = L_dyn + (c & 1u) * IMGW + 4u;
 		if (LBC == 1 && c == 2u)
 			__syncthreads(); // chunk 0's image was stored (late) after the last barrier
 		if (c >= 2) {
@@ -957,7 +959,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			if (LBC == 0)
 				pred_c = seg_pred;
 			else if (tot_first) // chunk 0 waited for the look-back: store it now
-				store_chunk(&L[0][4], 0u, tot_first, seg_pred, is_last && last_ne == 0u);
+				store_chunk(L_dyn + 4u, 0u, tot_first, seg_pred, is_last && last_ne == 0u);
 		}
 
 		if (c >= LBC)
@@ -1360,7 +1362,8 @@ static uint32_t ensure_granules(airs_dev_engine *e, size_t segs)
 template <int W, int PRE, int ENC, bool RICE, int MODEL>
 static void launch_encode(const KArgs &k, uint32_t grid, hipStream_t s)
 {
-	hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL>), dim3(grid), dim3(AIRS_WG), 0, s, k);
+	const size_t lds = (size_t)2u * (k.img_words + 4u) * 4u;
+	hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL>), dim3(grid), dim3(AIRS_WG), lds, s, k);
 }
 
 template <int W, int PRE, int MODEL>
@@ -1460,6 +1463,26 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	k.enc_hdr = L->encoder_type;
 	k.model_rate_hdr = L->model_rate;
 	k.ticket_base = e->ticket_base;
+	{
+		// longest codeword (bits per sample) the pass can emit, which sizes the
+		// two LDS chunk images: UNCOMPRESSED 16; ZERO k+17 (escape, and the
+		// longest non-escape code) with k = floor(log2 g), 32 when g varies per
+		// frame; MULTI up to 48 (two pieces)
+		uint32_t maxbits = 48u;
+		if (L->encoder_type == ENC_RAW) {
+			maxbits = 16u;
+		} else if (L->encoder_type == ENC_ZERO) {
+			uint32_t kk = 15u;
+			if (!L->frame_g && L->encoder_param) {
+				kk = 0u;
+				while ((2u << kk) <= L->encoder_param && kk < 31u)
+					kk++;
+			}
+			maxbits = kk + 17u < 32u ? kk + 17u : 32u;
+		}
+		const uint32_t words = AIRS_SEG * maxbits / 32u + 4u;
+		k.img_words = (words + 3u) & ~3u;
+	}
 	e->epoch = (e->epoch + 1u) & 0x7FFFFFFFu;
 	if (e->epoch == 0)
 		e->epoch = 1;
