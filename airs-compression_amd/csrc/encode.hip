@@ -652,7 +652,10 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	}
 
 	// ---- the segment's last 32 bits (wave 3 rebuilds its last chunk) ------
-	constexpr int LB_WIN = 4; // look-back windows of 64 granules fetched per round
+#ifndef AIRS_LB_WIN
+#define AIRS_LB_WIN 2
+#endif
+	constexpr int LB_WIN = AIRS_LB_WIN; // look-back windows of 64 granules fetched per round
 	uint64_t gv[LB_WIN];
 #pragma unroll
 	for (int w = 0; w < LB_WIN; w++)
