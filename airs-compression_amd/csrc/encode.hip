@@ -827,13 +827,26 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 						for (uint32_t h = 0; h < 2; h++)
 							te[2 * jj + h] = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
 					}
+					// both codewords of a pair go in one put when they fit in 32
+					// bits (almost always); a longer pair takes two
 #pragma unroll
-					for (uint32_t i = 0; i < AIRS_PT / 2; i++) {
+					for (uint32_t i = 0; i < AIRS_PT / 2; i += 2) {
 						const uint32_t j = hb * (AIRS_PT / 2) + i;
-						pk1.put(half16(mp[0][j >> 1], j & 1u) + te[i].x, te[i].y);
+						const uint32_t cwa = (mp[0][j >> 1] & 0xFFFFu) + te[i].x;
+						const uint32_t cwb = (mp[0][j >> 1] >> 16) + te[i + 1].x;
+						const uint32_t lab = te[i].y + te[i + 1].y;
+						if (lab <= 32u) {
+							pk1.put((cwa << te[i + 1].y) | cwb, lab);
+						} else {
+							pk1.put(cwa, te[i].y);
+							pk1.put(cwb, te[i + 1].y);
+						}
 						ln[0][j] = te[i].y;
-						if (NPIECE == 2)
+						ln[0][j + 1] = te[i + 1].y;
+						if (NPIECE == 2) {
 							ln[NPIECE - 1][j] = 0u;
+							ln[NPIECE - 1][j + 1] = 0u;
+						}
 					}
 				}
 			} else {
