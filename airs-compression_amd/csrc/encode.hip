@@ -336,47 +336,43 @@ __device__ __forceinline__ RicePair rice_pair(uint32_t m2, uint32_t k, uint32_t 
 	return r;
 }
 
-// Bit packer into an LDS image.  `nb` is the absolute bit position inside
-// the image; acc holds (at least) the last 32 + (nb mod 32) bits.  Every put
-// ORs the 32 bits that precede the pending ones into their word: when a word
-// just completed that is the new word, otherwise it is the previous word
-// again (or zeros before the lane's first bit), which ORs nothing new.  So
-// there is one ds_or per piece and no select or branch.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// Bit packer into an LDS image.  `nb` is a bit position in the LDS address
+// space: 8 * (byte address of the image) + (bit offset inside the image) - 32,
+// so the word that holds the 32 bits preceding the pending ones is at byte
+// address (nb >> 3) & ~3 (no base add per step) and nb mod 32 is the pending
+// count.  acc holds (at least) the last 32 + (nb mod 32) bits.  Every put ORs
+// those preceding 32 bits into their word: when a word just completed that is
+// the new word, otherwise it is the previous word again (or zeros before the
+// lane's first bit), which ORs nothing new.  So there is one ds_or per piece
+// and no select or branch.
 struct Packer {
 	uint64_t acc;
 	uint32_t nb;
-	uint32_t *img;
-#if defined(AIRS_EXP_SINK)
-	uint32_t sink = 0u;
-#endif
 
-	__device__ __forceinline__ void init(uint32_t *image, uint32_t bit)
+	__device__ __forceinline__ void init(const uint32_t *image, uint32_t bit)
 	{
 		acc = 0u;
-		nb = bit;
-		img = image;
+		// the low 32 bits of a generic LDS pointer are its LDS byte address
+		nb = ((uint32_t)(uintptr_t)image << 3) + bit - 32u;
 	}
 	__device__ __forceinline__ void put(uint32_t cw, uint32_t len) // len <= 32, cw < 2^len
 	{
 		acc = (acc << len) | cw;
 		nb += len;
 		// v_alignbit uses nb mod 32
-#if defined(AIRS_EXP_SINK)
-		sink ^= __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, nb) + (uint32_t)(uintptr_t)(img + __builtin_amdgcn_ubfe(nb, 5u, 27u) - 1);
-#elif defined(AIRS_EXP_WRITE)
-		img[__builtin_amdgcn_ubfe(nb, 5u, 27u) - 1] = __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, nb);
-#else
-		atomicOr(img + __builtin_amdgcn_ubfe(nb, 5u, 27u) - 1,
-			 __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, nb));
-#endif
+		lds_u32 *w = reinterpret_cast<lds_u32 *>((uintptr_t)((nb >> 3) & ~3u));
+		__hip_atomic_fetch_or(w, __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, nb),
+				      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 	}
 	__device__ __forceinline__ void flush()
 	{
-#if defined(AIRS_EXP_SINK)
-		atomicOr(img + (nb >> 5), sink);
-#endif
-		if (nb & 31u)
-			atomicOr(img + (nb >> 5), (uint32_t)acc << (32u - (nb & 31u)));
+		if (nb & 31u) {
+			lds_u32 *w = reinterpret_cast<lds_u32 *>((uintptr_t)(((nb >> 3) & ~3u) + 4u));
+			__hip_atomic_fetch_or(w, (uint32_t)acc << (32u - (nb & 31u)), __ATOMIC_RELAXED,
+					      __HIP_MEMORY_SCOPE_WORKGROUP);
+		}
 	}
 };
 
