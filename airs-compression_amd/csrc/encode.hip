@@ -445,6 +445,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	__shared__ __attribute__((aligned(16))) uint2 s_rice[20];
 
 	const uint32_t tid = threadIdx.x, lane = tid & 63u;
+	if (a.dbg & 16384u) // ablation: empty kernel
+		return;
 	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform
 
 	// ---- segment id: dispatch order (or an atomic ticket, debug switch) ----
@@ -488,9 +490,16 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		const bool full = firstc[c] + AIRS_PT <= n;
 		if (full && src_al) {
 			const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)firstc[c] * W);
+			if (a.dbg & 512u) { // ablation: no HBM reads (synthetic in-register data)
 #pragma unroll
-			for (uint32_t q = 0; q < RW; q++)
-				raw[c][q] = p[q];
+				for (uint32_t q = 0; q < RW; q++)
+					raw[c][q] = make_uint4(0x40004000u + tid * 3u + q, 0x40104008u + c, 0x40204010u ^ tid,
+							       0x40304018u + q * 7u);
+			} else {
+#pragma unroll
+				for (uint32_t q = 0; q < RW; q++)
+					raw[c][q] = p[q];
+			}
 		}
 		if (MODEL == 2 && full && mod_al) {
 			const uint4 *p = reinterpret_cast<const uint4 *>(fmodel + (size_t)firstc[c] * 2u);
@@ -498,7 +507,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			mraw[c][1] = p[1];
 		}
 		prevld[c] = 0u;
-		if (PRE == PRE_DIFF && lane == 0u && firstc[c] != 0u && firstc[c] <= n)
+		if (PRE == PRE_DIFF && lane == 0u && firstc[c] != 0u && firstc[c] <= n && !(a.dbg & 512u))
 			prevld[c] = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fsrc)[firstc[c] - 1u]
 					   : reinterpret_cast<const uint32_t *>(fsrc)[firstc[c] - 1u] & 0xFFFFu;
 	}
@@ -506,7 +515,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// zero both LDS chunk images while the loads are in flight
 	{
 		uint4 *L4 = reinterpret_cast<uint4 *>(L_dyn);
-		for (uint32_t i = tid; i < 2u * IMGW / 4u; i += AIRS_WG)
+		for (uint32_t i = tid; i < ((a.dbg & 4096u) ? 0u : 2u * IMGW / 4u); i += AIRS_WG)
 			L4[i] = make_uint4(0u, 0u, 0u, 0u);
 	}
 
@@ -594,7 +603,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				u = unpk(pk(w[j]) - pk(pm[j]));
 			else
 				u = w[j];
-			mp[c][j] = ENC == ENC_RAW ? u : zigzag_pk(u);
+			mp[c][j] = (a.dbg & 8192u) ? w[j] : (ENC == ENC_RAW ? u : zigzag_pk(u));
 		}
 		uint32_t t = 0u;
 		if (a.dbg & 64u) {
@@ -638,6 +647,11 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			asm volatile("" : "+v"(mp[c][i]));
 	}
 
+	if (a.dbg & 32768u) { // ablation: stop after phase 1
+		if (T[0] == 0x12345u && tid == 999u)
+			a.status[0] = mp[0][0] + mp[CH - 1][1];
+		return;
+	}
 	// ---- per-chunk block scans (DPP within waves, LDS across waves) -------
 	uint32_t inc[CH];
 #pragma unroll
@@ -753,10 +767,11 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		const uint32_t endbit = Pc + totx;
 		const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
 		const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
-		for (uint32_t j = tid; j < nfull; j += AIRS_WG) {
+		for (uint32_t j = tid; j < ((a.dbg & 2048u) ? 0u : nfull); j += AIRS_WG) {
 			const uint32_t hi = j ? Lx[j - 1u] : predx;
 			const uint32_t v = __builtin_amdgcn_alignbit(hi, Lx[j], r);
-			__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
+			if (!(a.dbg & 1024u)) // ablation: no HBM writes
+				__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
 		}
 		if (finalx && nfull == J && tid == 0) {
 			// zero-padded final bytes of the payload (reference bitstream_flush)
@@ -775,7 +790,10 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// always index 0 of mp/nmp/nv/excl/tot/base/firstc, rotated at the end
 	uint32_t tot_m2 = 0u; // total of chunk c-2 (its image is recycled now)
 	uint32_t tot_m1 = 0u;
-#pragma unroll 1
+#ifndef AIRS_CHUNK_UNROLL
+#define AIRS_CHUNK_UNROLL 1
+#endif
+#pragma unroll AIRS_CHUNK_UNROLL
 	for (uint32_t c = 0; c < CH; c++) {
 		uint32_t *Lc = L_dyn + (c & 1u) * IMGW + 4u;
 		if (LBC == 1 && c == 2u)
@@ -784,7 +802,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			// image c&1 was last read by chunk c-2's stores (before the barrier
 			// that ended chunk c-1's packing): clear what it used
 			const uint32_t nw = (max(tot_m2, tot[0]) + 31u) >> 5;
-			for (uint32_t i = tid; i <= nw; i += AIRS_WG)
+			for (uint32_t i = tid; i <= ((a.dbg & 4096u) ? 0u : nw); i += AIRS_WG)
 				Lc[i] = 0u;
 			__syncthreads();
 		}
