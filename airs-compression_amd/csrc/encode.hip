@@ -296,6 +296,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 // values of a lane's 16 samples travel as 8 packed registers.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ u16x2 pk(uint32_t x)
 {
@@ -767,10 +768,27 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		const uint32_t endbit = Pc + totx;
 		const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
 		const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
-		for (uint32_t j = tid; j < ((a.dbg & 2048u) ? 0u : nfull); j += AIRS_WG) {
-			const uint32_t hi = j ? Lx[j - 1u] : predx;
-			const uint32_t v = __builtin_amdgcn_alignbit(hi, Lx[j], r);
+		// two words per thread: one 8-byte LDS read + its left neighbour, one
+		// 8-byte buffer store (the image is 8-byte aligned, j even)
+		const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)Lx);
+		const uint32_t npair = (a.dbg & 2048u) ? 0u : (nfull >> 1);
+		for (uint32_t p = tid; p < npair; p += AIRS_WG) {
+			const uint32_t j = 2u * p;
+			const u32x2 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x2 *>(Ll + j);
+			const uint32_t hi = j ? Ll[j - 1u] : predx;
+			u32x2 o;
+			o.x = bswap32(__builtin_amdgcn_alignbit(hi, w.x, r));
+			o.y = bswap32(__builtin_amdgcn_alignbit(w.x, w.y, r));
 			if (!(a.dbg & 1024u)) // ablation: no HBM writes
+				__builtin_amdgcn_raw_buffer_store_b64(o, dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
+		}
+		// odd last word: the thread next in turn (thread 0 when it is word 0,
+		// the only one that needs predx, which lives in lane 0 of wave 0)
+		if ((nfull & 1u) && tid == (npair & (AIRS_WG - 1u)) && !(a.dbg & 2048u)) {
+			const uint32_t j = nfull - 1u;
+			const uint32_t hi = j ? Ll[j - 1u] : predx;
+			const uint32_t v = __builtin_amdgcn_alignbit(hi, Ll[j], r);
+			if (!(a.dbg & 1024u))
 				__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
 		}
 		if (finalx && nfull == J && tid == 0) {
