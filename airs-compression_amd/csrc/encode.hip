@@ -297,6 +297,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ u16x2 pk(uint32_t x)
 {
@@ -768,24 +769,28 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		const uint32_t endbit = Pc + totx;
 		const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
 		const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
-		// two words per thread: one 8-byte LDS read + its left neighbour, one
-		// 8-byte buffer store (the image is 8-byte aligned, j even)
+		// four words per thread: one 16-byte LDS read + its left neighbour, one
+		// 16-byte buffer store (the image is 16-byte aligned, j a multiple of 4)
 		const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)Lx);
-		const uint32_t npair = (a.dbg & 2048u) ? 0u : (nfull >> 1);
-		for (uint32_t p = tid; p < npair; p += AIRS_WG) {
-			const uint32_t j = 2u * p;
-			const u32x2 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x2 *>(Ll + j);
+		const uint32_t nquad = (a.dbg & 2048u) ? 0u : (nfull >> 2);
+		for (uint32_t p = tid; p < nquad; p += AIRS_WG) {
+			const uint32_t j = 4u * p;
+			const u32x4 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + j);
 			const uint32_t hi = j ? Ll[j - 1u] : predx;
-			u32x2 o;
+			u32x4 o;
 			o.x = bswap32(__builtin_amdgcn_alignbit(hi, w.x, r));
 			o.y = bswap32(__builtin_amdgcn_alignbit(w.x, w.y, r));
+			o.z = bswap32(__builtin_amdgcn_alignbit(w.y, w.z, r));
+			o.w = bswap32(__builtin_amdgcn_alignbit(w.z, w.w, r));
 			if (!(a.dbg & 1024u)) // ablation: no HBM writes
-				__builtin_amdgcn_raw_buffer_store_b64(o, dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
+				__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
 		}
-		// odd last word: the thread next in turn (thread 0 when it is word 0,
-		// the only one that needs predx, which lives in lane 0 of wave 0)
-		if ((nfull & 1u) && tid == (npair & (AIRS_WG - 1u)) && !(a.dbg & 2048u)) {
-			const uint32_t j = nfull - 1u;
+		// the last nfull % 4 words: one each for the threads next in turn
+		// (thread 0 when one of them is word 0, the only word that needs
+		// predx, which lives in lane 0 of wave 0)
+		const uint32_t rr = (tid - nquad) & (AIRS_WG - 1u);
+		if (rr < (nfull & 3u) && !(a.dbg & 2048u)) {
+			const uint32_t j = 4u * nquad + rr;
 			const uint32_t hi = j ? Ll[j - 1u] : predx;
 			const uint32_t v = __builtin_amdgcn_alignbit(hi, Ll[j], r);
 			if (!(a.dbg & 1024u))
