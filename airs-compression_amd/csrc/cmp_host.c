@@ -198,16 +198,28 @@ static int model_needed(const struct cmp_params *p)
 	return p->secondary_preprocessing == CMP_PREPROCESS_MODEL && p->secondary_iterations != 0;
 }
 
-uint32_t cmp_reset(struct cmp_context *ctx)
+/* cmp_reset; with `draws` set the identifier draw is only counted (the batch
+ * API draws the identifiers afterwards, in the reference's call order) */
+static uint32_t ctx_reset(struct cmp_context *ctx, uint32_t *draws)
 {
 	if (!ctx)
 		return ERRV(GENERIC);
 	if (ctx->magic != CTX_MAGIC)
 		return ERRV(CONTEXT_INVALID);
 	ctx->sequence_number = 0;
-	ctx->identifier = next_identifier();
+	if (draws) {
+		(*draws)++;
+		ctx->identifier = 0;
+	} else {
+		ctx->identifier = next_identifier();
+	}
 	ctx->model_size = 0;
 	return ERRV(NO_ERROR);
+}
+
+uint32_t cmp_reset(struct cmp_context *ctx)
+{
+	return ctx_reset(ctx, NULL);
 }
 
 void cmp_deinitialise(struct cmp_context *ctx)
@@ -282,7 +294,7 @@ struct pass {
 	uint32_t hdr_bytes;
 };
 
-enum { SLOT_SRC = 0, SLOT_DST, SLOT_MODEL, SLOT_STATUS, SLOT_CK, SLOT_IDS, SLOT_G, SLOT_AUX };
+enum { SLOT_SRC = 0, SLOT_DST, SLOT_MODEL, SLOT_STATUS, SLOT_CK, SLOT_IDS, SLOT_G, SLOT_AUX, SLOT_FL, SLOT_SIZES };
 
 static struct airs_dev_engine *g_host_dev;
 
@@ -299,14 +311,15 @@ static struct airs_dev_engine *host_dev(void)
 
 /* checks and state updates of compress_engine up to the encode loop;
  * returns 0 (pass filled in) or the error the reference would return */
-static uint32_t engine_prologue(struct cmp_context *ctx, void *dst, uint32_t cap, uint32_t n, struct pass *p)
+static uint32_t engine_prologue(struct cmp_context *ctx, void *dst, uint32_t cap, uint32_t n, struct pass *p,
+			       uint32_t *draws)
 {
 	const uint32_t packed = 2u * n;
 	uint32_t e;
 
 	memset(p, 0, sizeof(*p));
 	if (ctx->sequence_number == 0 || ctx->sequence_number > ctx->params.secondary_iterations) {
-		e = cmp_reset(ctx);
+		e = ctx_reset(ctx, draws);
 		if (is_err(e))
 			return e;
 		p->pre = ctx->params.primary_preprocessing;
@@ -389,7 +402,7 @@ static uint32_t host_engine(struct cmp_context *ctx, void *dst, uint32_t cap, co
 	const uint32_t packed = 2u * io->n;
 	void *d_src, *d_dst, *d_model = NULL, *d_status, *d_ck = NULL;
 
-	e = engine_prologue(ctx, dst, cap, io->n, &p);
+	e = engine_prologue(ctx, dst, cap, io->n, &p, NULL);
 	if (is_err(e))
 		return e;
 	dev = host_dev();
@@ -607,24 +620,50 @@ static int affine_u64(const uint64_t *v, uint32_t cnt, uint64_t *step)
 	return 1;
 }
 
-/* launch the frames j -> batch frame (add + j*mul), j < cnt, all with pass P */
+/* Launch cnt frames that share one pass: launch frame j is batch frame
+ * fl[j] (host list) or add + j*mul; output capacity cap. */
 static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t fpc,
-			     const struct cmp_gpu_batch *b, const struct frame_plan *plan, uint32_t add,
-			     uint32_t mul, uint32_t cnt, uint64_t *ids_scratch, uint64_t *ptr_scratch)
+			     const struct cmp_gpu_batch *b, const struct frame_plan *plan, const uint32_t *fl,
+			     uint32_t add, uint32_t mul, uint32_t cnt, uint32_t cap, uint64_t *ids_scratch,
+			     uint64_t *ptr_scratch)
 {
 	struct airs_dev_engine *dev = eng->dev;
-	const struct pass *P = &plan[add].p;
-	const struct cmp_params *prm = &ctx[add / fpc].params;
+	const uint32_t f0 = fl ? fl[0] : add;
+	const struct pass *P = &plan[f0].p;
+	const struct cmp_params *prm = &ctx[f0 / fpc].params;
 	const uint32_t bytes = b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
 	const uint32_t n = b->src_size / bytes;
-	const uint32_t nframes_total = (add + (cnt - 1) * mul) + 1;
+	uint32_t nframes_total = 0;
 	struct airs_launch L;
 	uint64_t step, worst = frame_worst(n);
-	uint32_t j, e, *d_g = NULL, *d_ck = NULL;
+	uint32_t j, e, *d_g = NULL, *d_ck = NULL, *d_fl = NULL;
 
+#define FRAME_AT(jj) (fl ? fl[jj] : add + (jj) * mul)
 	memset(&L, 0, sizeof(L));
-	for (j = 0; j < cnt; j++)
-		ids_scratch[j] = plan[add + j * mul].id;
+	if (fl) {
+		/* an affine list launches without a device copy */
+		uint32_t aff = 1, m = cnt > 1 ? fl[1] - fl[0] : 1;
+
+		for (j = 1; j < cnt && aff; j++)
+			aff = fl[j] == fl[0] + j * m;
+		if (aff) {
+			add = fl[0];
+			mul = m;
+			fl = NULL;
+		}
+	}
+	for (j = 0; j < cnt; j++) {
+		const uint32_t f = FRAME_AT(j);
+
+		ids_scratch[j] = plan[f].id;
+		if (f + 1u > nframes_total)
+			nframes_total = f + 1u;
+	}
+	if (fl) {
+		d_fl = airs_dev_scratch(dev, SLOT_FL, (size_t)cnt * 4u);
+		if (!d_fl || is_err(airs_dev_h2d(dev, d_fl, fl, (size_t)cnt * 4u)) || is_err(airs_dev_sync(dev)))
+			return ERRV(GENERIC);
+	}
 	if (affine_u64(ids_scratch, cnt, &step)) {
 		L.id_base = ids_scratch[0];
 		L.id_step = step;
@@ -638,7 +677,7 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 	}
 	if (P->model_mode != AIRS_MODEL_NONE) {
 		for (j = 0; j < cnt; j++)
-			ptr_scratch[j] = (uint64_t)(uintptr_t)ctx[(add + j * mul) / fpc].work_buf;
+			ptr_scratch[j] = (uint64_t)(uintptr_t)ctx[FRAME_AT(j) / fpc].work_buf;
 		/* model of frame f = base + (f / fpc) * stride when the work buffers are strided */
 		{
 			uint64_t base = (uint64_t)(uintptr_t)ctx[0].work_buf, mstep = 0;
@@ -662,13 +701,18 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 			}
 		}
 	}
+#undef FRAME_AT
 	if (prm->checksum_enabled) {
 		d_ck = airs_dev_scratch(dev, SLOT_CK, (size_t)nframes_total * 4u);
 		if (!d_ck)
 			return ERRV(GENERIC);
-		/* the checksum kernel takes a frame list: reuse the affine map via a
-		 * contiguous range when mul == 1, else hash every frame up to the last */
-		e = airs_dev_checksum(dev, b->src, b->src_stride, bytes, n, nframes_total, NULL, d_ck);
+		if (fl)
+			e = airs_dev_checksum(dev, b->src, b->src_stride, bytes, n, cnt, d_fl, d_ck);
+		else if (mul == 1)
+			e = airs_dev_checksum(dev, (const uint8_t *)b->src + (uint64_t)add * b->src_stride,
+					      b->src_stride, bytes, n, cnt, NULL, d_ck + add);
+		else
+			e = airs_dev_checksum(dev, b->src, b->src_stride, bytes, n, nframes_total, NULL, d_ck);
 		if (is_err(e))
 			return e;
 	}
@@ -686,11 +730,12 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 	L.is_unsigned = b->type == CMP_GPU_U16;
 	L.n = n;
 	L.num_frames = cnt;
+	L.frame_list = d_fl;
 	L.frame_add = add;
 	L.frame_mul = mul;
 	L.dst = b->dst;
 	L.dst_stride = b->dst_stride;
-	L.cap = (uint64_t)b->dst_capacity < worst ? b->dst_capacity : (uint32_t)worst;
+	L.cap = (uint64_t)cap < worst ? cap : (uint32_t)worst;
 	L.preprocessing = P->pre;
 	L.encoder_type = P->enc;
 	L.encoder_param = P->par;
@@ -698,7 +743,7 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 	L.frame_g = d_g;
 	L.model_mode = P->model_mode;
 	L.model_rate = prm->model_rate;
-	L.fail_bit = model_fail_bit(b->dst_capacity, n);
+	L.fail_bit = model_fail_bit(cap, n);
 	L.seq = P->seq;
 	L.checksum_enabled = prm->checksum_enabled ? 1u : 0u;
 	L.checksums = d_ck;
@@ -706,11 +751,195 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 	return airs_dev_encode(dev, &L);
 }
 
+/* size of the raw (fallback) frame of a context, as cmp_compress_generic (cmp.c:342-393) */
+static uint32_t raw_frame_size(const struct cmp_context *ctx, uint32_t n)
+{
+	return CMP_HDR_SIZE + 2u * n + (ctx->params.checksum_enabled ? CMP_CHECKSUM_SIZE : 0u);
+}
+
+/* launch every frame of `list` (batch frames of one acquisition step): one
+ * launch per run of frames with the same pass and capacity */
+static uint32_t launch_groups(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t fpc,
+			      const struct cmp_gpu_batch *b, const struct frame_plan *plan, const uint32_t *list,
+			      const uint32_t *caps, uint32_t cnt, uint32_t *grp, uint8_t *done, uint64_t *ids,
+			      uint64_t *ptrs)
+{
+	uint32_t i, k, e = 0;
+
+	memset(done, 0, cnt);
+	for (i = 0; i < cnt && !is_err(e); i++) {
+		uint32_t g = 0;
+
+		if (done[i])
+			continue;
+		for (k = i; k < cnt; k++) {
+			if (!done[k] && caps[k] == caps[i] && same_pass(&plan[list[k]].p, &plan[list[i]].p) &&
+			    ctx[list[k] / fpc].params.model_rate == ctx[list[i] / fpc].params.model_rate &&
+			    ctx[list[k] / fpc].params.checksum_enabled == ctx[list[i] / fpc].params.checksum_enabled) {
+				grp[g++] = list[k];
+				done[k] = 1;
+			}
+		}
+		e = batch_launch(eng, ctx, fpc, b, plan, grp, 0, 1, g, caps[i], ids, ptrs);
+	}
+	return e;
+}
+
+/*
+ * Exact mode: one acquisition step at a time, as the host API would run it.
+ * Used when a frame can fail or fall back to raw storage, because the
+ * outcome of frame (c, a) decides the pass (and identifier draws) of frame
+ * (c, a+1).  Per step: plan every context, launch, read the sizes back, run
+ * the fallback frames (cmp_compress_generic: reset, NONE + UNCOMPRESSED at
+ * the raw size), and advance the contexts that succeeded.  Identifier draws
+ * are counted per frame and made at the end in the reference's call order
+ * (context-major), then written into the headers.
+ */
+static uint32_t batch_exact(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx, uint32_t fpc,
+			    const struct cmp_gpu_batch *b, struct frame_plan *plan, uint64_t *ids, uint64_t *ptrs)
+{
+	struct airs_dev_engine *dev = eng->dev;
+	const uint32_t bytes = b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
+	const uint32_t n = b->src_size / bytes, total = num_ctx * fpc;
+	uint32_t *draws = calloc(total, sizeof(uint32_t));
+	uint32_t *list = calloc(num_ctx, sizeof(uint32_t)), *caps = calloc(num_ctx, sizeof(uint32_t));
+	uint32_t *grp = calloc(num_ctx, sizeof(uint32_t)), *sz = calloc(num_ctx, sizeof(uint32_t));
+	uint32_t *fbl = calloc(num_ctx, sizeof(uint32_t)), *fbc = calloc(num_ctx, sizeof(uint32_t));
+	uint32_t *perr = calloc(num_ctx, sizeof(uint32_t));
+	uint64_t *id0 = calloc(num_ctx, sizeof(uint64_t));
+	uint8_t *done = calloc(num_ctx, 1);
+	uint32_t a, c, e = 0;
+
+	if (!draws || !list || !caps || !grp || !sz || !fbl || !fbc || !perr || !id0 || !done) {
+		e = ERRV(GENERIC);
+		goto out;
+	}
+	for (c = 0; c < num_ctx; c++)
+		id0[c] = ctx[c].identifier;
+	for (a = 0; a < fpc && !is_err(e); a++) {
+		uint32_t nfb = 0, nl = 0;
+
+		for (c = 0; c < num_ctx && !is_err(e); c++) {
+			const uint32_t f = c * fpc + a, raw = raw_frame_size(&ctx[c], n);
+			void *dst = (uint8_t *)b->dst + (uint64_t)f * b->dst_stride;
+
+			const uint32_t cap = ctx[c].params.uncompressed_fallback_enabled && b->dst_capacity >= raw
+						     ? raw
+						     : b->dst_capacity;
+			/* a frame the host API rejects before encoding keeps its error */
+			perr[c] = engine_prologue(&ctx[c], dst, cap, n, &plan[f].p, &draws[f]);
+			plan[f].id = 0; /* written at the end */
+			if (is_err(perr[c])) {
+				e = airs_dev_h2d(dev, b->sizes + f, &perr[c], 4u);
+			} else {
+				list[nl] = f;
+				caps[nl++] = cap;
+			}
+		}
+		if (is_err(e))
+			break;
+		if (nl)
+			e = launch_groups(eng, ctx, fpc, b, plan, list, caps, nl, grp, done, ids, ptrs);
+		if (is_err(e))
+			break;
+		/* sizes of this step (frames c*fpc + a: strided in the sizes array) */
+		for (c = 0; c < num_ctx && !is_err(e); c++) {
+			sz[c] = perr[c];
+			if (!is_err(perr[c]))
+				e = airs_dev_d2h(dev, &sz[c], b->sizes + (uint64_t)c * fpc + a, 4u);
+		}
+		if (is_err(e) || is_err(e = airs_dev_sync(dev)))
+			break;
+		for (c = 0; c < num_ctx && !is_err(e); c++) {
+			const uint32_t f = c * fpc + a, raw = raw_frame_size(&ctx[c], n);
+			enum cmp_preprocessing save_pre;
+			enum cmp_encoder_type save_enc;
+			void *dst = (uint8_t *)b->dst + (uint64_t)f * b->dst_stride;
+
+			/* sz[c] holds the prologue's error when the frame was rejected
+			 * before encoding (e.g. raw size below the compressed header) */
+			if (!(ctx[c].params.uncompressed_fallback_enabled && b->dst_capacity >= raw &&
+			      cmp_get_error_code(sz[c]) == CMP_ERR_DST_TOO_SMALL))
+				continue;
+			/* cmp.c:342-393: reset, then the frame again as NONE + UNCOMPRESSED */
+			e = ctx_reset(&ctx[c], &draws[f]);
+			if (is_err(e))
+				break;
+			save_pre = ctx[c].params.primary_preprocessing;
+			save_enc = ctx[c].params.primary_encoder_type;
+			ctx[c].params.primary_preprocessing = CMP_PREPROCESS_NONE;
+			ctx[c].params.primary_encoder_type = CMP_ENCODER_UNCOMPRESSED;
+			perr[c] = engine_prologue(&ctx[c], dst, raw, n, &plan[f].p, &draws[f]);
+			ctx[c].params.primary_preprocessing = save_pre;
+			ctx[c].params.primary_encoder_type = save_enc;
+			plan[f].id = 0;
+			if (is_err(perr[c])) {
+				sz[c] = perr[c];
+				e = airs_dev_h2d(dev, b->sizes + f, &perr[c], 4u);
+				continue;
+			}
+			fbl[nfb] = f;
+			fbc[nfb++] = raw;
+		}
+		if (is_err(e))
+			break;
+		if (nfb) {
+			e = launch_groups(eng, ctx, fpc, b, plan, fbl, fbc, nfb, grp, done, ids, ptrs);
+			for (c = 0; c < nfb && !is_err(e); c++)
+				e = airs_dev_d2h(dev, &sz[fbl[c] / fpc], b->sizes + fbl[c], 4u);
+			if (is_err(e) || is_err(e = airs_dev_sync(dev)))
+				break;
+		}
+		for (c = 0; c < num_ctx; c++)
+			if (!is_err(sz[c]))
+				ctx[c].sequence_number++;
+	}
+	if (is_err(e))
+		goto out;
+	/* identifiers in call order; frames without a draw carry the context's */
+	{
+		uint64_t *d_ids;
+
+		for (c = 0; c < num_ctx; c++) {
+			uint64_t id = id0[c];
+
+			for (a = 0; a < fpc; a++) {
+				const uint32_t f = c * fpc + a;
+				uint32_t k;
+
+				for (k = 0; k < draws[f]; k++)
+					id = next_identifier();
+				ids[f] = id;
+			}
+			ctx[c].identifier = id;
+		}
+		d_ids = airs_dev_scratch(dev, SLOT_IDS, (size_t)total * 8u);
+		if (!d_ids || is_err(airs_dev_h2d(dev, d_ids, ids, (size_t)total * 8u)))
+			e = ERRV(GENERIC);
+		else
+			e = airs_dev_patch_ids(dev, b->dst, b->dst_stride, total, 0, 1, d_ids, b->sizes);
+		if (!is_err(e))
+			e = airs_dev_sync(dev);
+	}
+out:
+	free(draws);
+	free(list);
+	free(caps);
+	free(grp);
+	free(sz);
+	free(fbl);
+	free(fbc);
+	free(perr);
+	free(id0);
+	free(done);
+	return e;
+}
+
 uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx,
 			  uint32_t fpc, const struct cmp_gpu_batch *b)
 {
 	const uint32_t bytes = b && b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
-	uint32_t n, c, a, total, e = 0, any_model = 0;
+	uint32_t n, c, a, total, e = 0, any_model = 0, exact = 0;
 	struct frame_plan *plan;
 	uint64_t *ids, *ptrs;
 
@@ -744,12 +973,8 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		if (ctx[c].magic != CTX_MAGIC)
 			return ERRV(CONTEXT_INVALID);
 		if (ctx[c].params.uncompressed_fallback_enabled &&
-		    b->dst_capacity >= CMP_HDR_SIZE + 2u * n + (ctx[c].params.checksum_enabled ? 4u : 0u)) {
-			/* fallback needs the exact frame-by-frame protocol */
-			fprintf(stderr, "airscmp: cmp_gpu_compress: uncompressed_fallback_enabled is not "
-					"supported by the batch API yet; use cmp_compress_*\n");
-			return ERRV(PARAMS_INVALID);
-		}
+		    b->dst_capacity >= raw_frame_size(&ctx[c], n))
+			exact = 1;
 		if (model_needed(&ctx[c].params)) {
 			any_model = 1;
 			if ((uintptr_t)ctx[c].work_buf & 1u)
@@ -766,22 +991,60 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		free(ptrs);
 		return ERRV(GENERIC);
 	}
-	/* replay the context state machine in call order (c-major), assuming
-	 * every frame succeeds; this draws the identifiers in reference order */
-	for (c = 0; c < num_ctx && !e; c++) {
-		for (a = 0; a < fpc && !e; a++) {
-			struct frame_plan *fp = &plan[c * fpc + a];
-			void *dst = (uint8_t *)b->dst + (uint64_t)(c * fpc + a) * b->dst_stride;
+	/* a frame that can fail (capacity below the worst case) changes its
+	 * context's next pass: such batches run step by step */
+	if ((uint64_t)b->dst_capacity < HDR_MAX_SIZE + CMP_CHECKSUM_SIZE + payload_bound(2u * n))
+		exact = 1;
+	if (!exact) {
+		/* replay the context state machine in call order (c-major), counting
+		 * identifier draws; a frame the host API would reject sends the
+		 * batch to the step-by-step path with the contexts untouched */
+		struct cmp_context *snap = malloc((size_t)num_ctx * sizeof(*snap));
+		uint32_t *draws = calloc(total, sizeof(uint32_t));
 
-			e = engine_prologue(&ctx[c], dst, b->dst_capacity, n, &fp->p);
-			if (is_err(e))
-				break;
-			fp->id = ctx[c].identifier;
-			ctx[c].sequence_number++;
+		if (!snap || !draws) {
+			free(snap);
+			free(draws);
+			e = ERRV(GENERIC);
+			goto out;
 		}
+		memcpy(snap, ctx, (size_t)num_ctx * sizeof(*snap));
+		for (c = 0; c < num_ctx && !exact; c++) {
+			for (a = 0; a < fpc; a++) {
+				const uint32_t f = c * fpc + a;
+				void *dst = (uint8_t *)b->dst + (uint64_t)f * b->dst_stride;
+
+				if (is_err(engine_prologue(&ctx[c], dst, b->dst_capacity, n, &plan[f].p, &draws[f]))) {
+					exact = 1;
+					break;
+				}
+				ctx[c].sequence_number++;
+			}
+		}
+		if (exact) {
+			memcpy(ctx, snap, (size_t)num_ctx * sizeof(*snap));
+		} else {
+			/* the identifiers, drawn in call order */
+			for (c = 0; c < num_ctx; c++) {
+				uint64_t id = snap[c].identifier;
+
+				for (a = 0; a < fpc; a++) {
+					const uint32_t f = c * fpc + a;
+
+					for (uint32_t k = 0; k < draws[f]; k++)
+						id = next_identifier();
+					plan[f].id = id;
+				}
+				ctx[c].identifier = id;
+			}
+		}
+		free(snap);
+		free(draws);
 	}
-	if (is_err(e))
+	if (exact) {
+		e = batch_exact(eng, ctx, num_ctx, fpc, b, plan, ids, ptrs);
 		goto out;
+	}
 
 	/* launch: frames with equal passes share one launch; MODEL contexts
 	 * step through acquisitions in order (the model carries state) */
@@ -794,7 +1057,7 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 
 			while (g < total && same_pass(&plan[g].p, &plan[f].p))
 				g++;
-			e = batch_launch(eng, ctx, fpc, b, plan, f, 1, g - f, ids, ptrs);
+			e = batch_launch(eng, ctx, fpc, b, plan, NULL, f, 1, g - f, b->dst_capacity, ids, ptrs);
 			f = g;
 		}
 	} else {
@@ -803,22 +1066,28 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		for (f = 1; f < total && uniform; f++)
 			uniform = same_pass(&plan[f].p, &plan[0].p);
 		if (uniform && !any_model) {
-			e = batch_launch(eng, ctx, fpc, b, plan, 0, 1, total, ids, ptrs);
+			e = batch_launch(eng, ctx, fpc, b, plan, NULL, 0, 1, total, b->dst_capacity, ids, ptrs);
 		} else {
-			/* one launch per acquisition step across the contexts; MODEL
-			 * contexts carry state from one step to the next */
+			/* one launch per acquisition step across the contexts (one per
+			 * pass when contexts are in different states); MODEL contexts
+			 * carry state from one step to the next */
+			uint32_t *list = calloc(num_ctx, sizeof(uint32_t)), *caps = calloc(num_ctx, sizeof(uint32_t));
+			uint32_t *grp = calloc(num_ctx, sizeof(uint32_t));
+			uint8_t *done = calloc(num_ctx, 1);
+
+			if (!list || !caps || !grp || !done)
+				e = ERRV(GENERIC);
 			for (a = 0; a < fpc && !is_err(e); a++) {
-				for (c = 1; c < num_ctx; c++)
-					if (!same_pass(&plan[c * fpc + a].p, &plan[a].p))
-						break;
-				if (c < num_ctx) {
-					fprintf(stderr, "airscmp: cmp_gpu_compress: contexts in different "
-							"states cannot share a batch\n");
-					e = ERRV(PARAMS_INVALID);
-					break;
+				for (c = 0; c < num_ctx; c++) {
+					list[c] = c * fpc + a;
+					caps[c] = b->dst_capacity;
 				}
-				e = batch_launch(eng, ctx, fpc, b, plan, a, fpc, num_ctx, ids, ptrs);
+				e = launch_groups(eng, ctx, fpc, b, plan, list, caps, num_ctx, grp, done, ids, ptrs);
 			}
+			free(list);
+			free(caps);
+			free(grp);
+			free(done);
 		}
 	}
 out:

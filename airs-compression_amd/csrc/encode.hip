@@ -1324,8 +1324,8 @@ struct airs_dev_engine {
 	uint32_t *ticket;
 	uint32_t ticket_base;
 	uint32_t epoch;
-	void *scratch[8];
-	size_t scratch_cap[8];
+	void *scratch[AIRS_NSLOT];
+	size_t scratch_cap[AIRS_NSLOT];
 };
 
 extern "C" int airs_dev_available(void)
@@ -1367,7 +1367,7 @@ extern "C" void airs_dev_engine_destroy(struct airs_dev_engine *e)
 	(void)hipFree(e->agg);
 	(void)hipFree(e->tail);
 	(void)hipFree(e->ticket);
-	for (int i = 0; i < 8; i++)
+	for (int i = 0; i < AIRS_NSLOT; i++)
 		(void)hipFree(e->scratch[i]);
 	free(e);
 }
@@ -1379,7 +1379,7 @@ extern "C" void *airs_dev_engine_stream(struct airs_dev_engine *e)
 
 extern "C" void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes)
 {
-	if (slot < 0 || slot >= 8)
+	if (slot < 0 || slot >= AIRS_NSLOT)
 		return nullptr;
 	if (e->scratch_cap[slot] < bytes) {
 		(void)hipStreamSynchronize(e->stream);

@@ -64,11 +64,17 @@ uint32_t cmp_gpu_engine_create(struct cmp_gpu_engine **engine, void *hip_stream)
 void cmp_gpu_engine_destroy(struct cmp_gpu_engine *engine);
 
 /* Compress num_ctx * frames_per_ctx frames (see the ordering note above).
- * Returns CMP_ERR_NO_ERROR or a call-level error (validation, as the host API
- * would report it for the first frame).  Per-frame results land in
- * batch->sizes.  The call is asynchronous on the engine's stream unless a
- * context has uncompressed_fallback_enabled, in which case it synchronises
- * once per acquisition step to resolve fallbacks exactly. */
+ * Returns CMP_ERR_NO_ERROR or a call-level error (batch validation: NULL or
+ * misaligned pointers, bad sizes, invalid contexts).  Per-frame results,
+ * including frames cmp_compress_* would reject, land in batch->sizes.
+ *
+ * When no frame can fail (dst_capacity at least the worst-case frame:
+ * 26 bytes + 6 per sample) and no context can fall back to raw storage, the
+ * call is asynchronous on the engine's stream.  Otherwise the outcome of
+ * frame (c, a) decides the pass of frame (c, a+1), so the call runs one
+ * acquisition step at a time and synchronises after each step (and after
+ * the step's fallbacks, cmp.c:342-393).  Identifier draws are counted per
+ * frame and made at the end, in the loop's order. */
 uint32_t cmp_gpu_compress(struct cmp_gpu_engine *engine, struct cmp_context *ctx, uint32_t num_ctx,
 			  uint32_t frames_per_ctx, const struct cmp_gpu_batch *batch);
 

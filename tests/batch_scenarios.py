@@ -1,0 +1,105 @@
+"""Batch-API scenarios: cmp_gpu_compress against the c-major loop of
+cmp_compress_* calls it is defined to equal (include/cmp_gpu.h).
+
+`run_batch_host` runs any CmpLib (the oracle) frame by frame in call order;
+`run_batch_gpu` runs the same frames through one cmp_gpu_compress call on
+device buffers.  Both return the same observable tuple: per frame the return
+value and bytes, per context identifier / sequence number / model size and
+the work buffer (model).
+"""
+import random
+
+import numpy as np
+
+import scenarios
+
+
+def _ts_counter(start):
+    stamp = [start]
+
+    def ts():
+        stamp[0] += 1
+        return (stamp[0] >> 16, stamp[0] & 0xFFFF)
+    return ts
+
+
+def make_case(api, trial):
+    """Seeded batch case: params, kind, n, nctx, fpc, cap, per-frame sources."""
+    rng = random.Random(trial)
+    params = scenarios.make_params(api.CmpParams, rng, allow_iwt=False)
+    params.uncompressed_fallback_enabled = rng.choice([0, 1, 1])
+    kind = rng.choice(scenarios.KINDS)
+    n = rng.choice([1, 7, 64, 333, 4095, 4097, 9000])
+    nctx = rng.choice([1, 2, 3])
+    fpc = rng.choice([1, 3, 6])
+    raw = 16 + 2 * n + (4 if params.checksum_enabled else 0)
+    worst = 22 + 4 + 6 * n
+    cap = rng.choice([worst, raw, raw + 3, raw - 1, 22 + n, 40])
+    srcs = [scenarios.make_src(kind, n, rng, rng.choice([1, 50, 3000, 30000])) for _ in range(nctx * fpc)]
+    return params, kind, n, nctx, fpc, cap, srcs
+
+
+def _work_size(lib, api, params, nbytes):
+    w = lib.cal_work_buf_size(params, nbytes)
+    return 0 if api.is_error(w) else w
+
+
+def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000):
+    sb = 4 if kind == "i16_in_i32" else 2
+    lib.set_timestamp_func(_ts_counter(ts_start))
+    try:
+        wbs = _work_size(lib, api, params, n * sb)
+        ctxs = [api.CmpContext() for _ in range(nctx)]
+        wbs_bufs = [api.aligned_empty(max(wbs, 2), fill=0) for _ in range(nctx)]
+        for c in range(nctx):
+            r = lib.initialise(ctxs[c], params, wbs_bufs[c] if wbs else None, wbs)
+            assert not api.is_error(r), api.error_name(r)
+        frames = []
+        for c in range(nctx):
+            for a in range(fpc):
+                dst = api.aligned_empty(cap + 64, fill=0xAB)
+                r = lib.compress(kind, ctxs[c], dst, cap, srcs[c * fpc + a])
+                frames.append((r, bytes(dst[:r]) if not api.is_error(r) else None))
+        state = [(x.identifier, x.sequence_number, x.model_size, bytes(w[:wbs]))
+                 for x, w in zip(ctxs, wbs_bufs)]
+        return tuple(frames), tuple(state)
+    finally:
+        lib.set_timestamp_func(None)
+
+
+def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000):
+    import torch
+    sb = 4 if kind == "i16_in_i32" else 2
+    nf = nctx * fpc
+    stride = n * sb
+    host_src = np.concatenate([np.ascontiguousarray(s).view(np.uint8) for s in srcs])
+    src = torch.from_numpy(host_src).cuda()
+    dstride = (cap + 64 + 7) // 8 * 8
+    dst = torch.full((nf * dstride,), 0xAB, dtype=torch.uint8, device="cuda")
+    sizes = torch.zeros(nf, dtype=torch.int32, device="cuda")
+    lib.set_timestamp_func(_ts_counter(ts_start))
+    try:
+        wbs = _work_size(lib, api, params, stride)
+        wstride = (max(wbs, 2) + 15) // 16 * 16
+        work = torch.zeros(nctx * wstride, dtype=torch.uint8, device="cuda")
+        ctxs = (api.CmpContext * nctx)()
+        for c in range(nctx):
+            r = lib.initialise(ctxs[c], params, (work.data_ptr() + c * wstride) if wbs else None, wbs)
+            assert not api.is_error(r), api.error_name(r)
+        torch.cuda.synchronize()
+        r = eng.compress(ctxs, fpc, kind, src.data_ptr(), stride, stride, dst.data_ptr(), dstride, cap,
+                         sizes.data_ptr(), 0)
+        assert r == 0, api.error_name(r)
+        assert eng.synchronize() == 0
+        sz = sizes.cpu().numpy().astype(np.uint32)
+        host = dst.cpu().numpy()
+        wk = work.cpu().numpy()
+        frames = []
+        for f in range(nf):
+            s = int(sz[f])
+            frames.append((s, bytes(host[f * dstride:f * dstride + s]) if not api.is_error(s) else None))
+        state = [(ctxs[c].identifier, ctxs[c].sequence_number, ctxs[c].model_size,
+                  bytes(wk[c * wstride:c * wstride + wbs])) for c in range(nctx)]
+        return tuple(frames), tuple(state)
+    finally:
+        lib.set_timestamp_func(None)
