@@ -55,6 +55,7 @@ struct airs_launch {
 	uint64_t model_stride;
 	uint32_t model_div;
 	const uint64_t *model_ptrs;
+	uint32_t model_ptrs_al16; /* every model_ptrs[j] is 16-byte aligned (host-checked) */
 	uint32_t model_mode;     /* enum airs_model_mode */
 	uint32_t model_rate;
 	uint64_t fail_bit;       /* samples reaching this frame bit keep their old model */

@@ -698,6 +698,10 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 				    is_err(airs_dev_sync(dev)))
 					return ERRV(GENERIC);
 				L.model_ptrs = d_ptr;
+				L.model_ptrs_al16 = 1;
+				for (j = 0; j < cnt; j++)
+					if (ptr_scratch[j] & 15u)
+						L.model_ptrs_al16 = 0;
 			}
 		}
 	}

@@ -49,6 +49,14 @@
 // engine->ticket[AIRS_FAULT_WORD] counts look-back give-ups (must stay 0)
 #define AIRS_FAULT_WORD 16
 
+// Ablation switches (AIRS_DBG bits, benchmarking only) are compiled in only
+// with -DAIRS_ABLATE=1: in the product build every DBG() is a constant false,
+// so the checks cost no instructions.
+#ifndef AIRS_ABLATE
+#define AIRS_ABLATE 0
+#endif
+#define DBG(bits) (AIRS_ABLATE && (a.dbg & (bits)))
+
 #define ERRV(code) ((uint32_t)0u - (uint32_t)(code))
 #define E_GENERIC 1u
 #define E_PARAMS_INVALID 10u
@@ -418,7 +426,7 @@ __host__ __device__ constexpr uint32_t seg_chunks(int W, int MODEL)
 	return (W == 4 || MODEL) ? 2u : 4u;
 }
 
-template <int W, int PRE, int ENC, bool RICE, int MODEL>
+template <int W, int PRE, int ENC, bool RICE, int MODEL, bool FULL>
 __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 {
 	constexpr uint32_t CH = seg_chunks(W, MODEL);
@@ -447,13 +455,13 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	__shared__ __attribute__((aligned(16))) uint2 s_rice[20];
 
 	const uint32_t tid = threadIdx.x, lane = tid & 63u;
-	if (a.dbg & 16384u) // ablation: empty kernel
+	if (DBG(16384u)) // ablation: empty kernel
 		return;
 	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform
 
 	// ---- segment id: dispatch order (or an atomic ticket, debug switch) ----
 	uint32_t seg = blockIdx.x;
-	if (a.dbg & 4u) {
+	if (DBG(4u)) {
 		if (tid == 0)
 			s_misc[0] = atomicAdd(a.ticket, 1u) - a.ticket_base;
 		__syncthreads();
@@ -478,8 +486,10 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	if (MODEL)
 		fmodel = a.model_ptrs ? reinterpret_cast<uint8_t *>(a.model_ptrs[lf])
 				      : a.model + (uint64_t)(frame / a.model_div) * a.model_stride;
-	const bool src_al = ((uintptr_t)fsrc & 15u) == 0;
-	const bool mod_al = MODEL ? ((uintptr_t)fmodel & 15u) == 0 : true;
+	// FULL launches (host-checked): every segment is whole and every frame and
+	// model base is 16-byte aligned, so no per-lane bounds or alignment tests
+	const bool src_al = FULL || ((uintptr_t)fsrc & 15u) == 0;
+	const bool mod_al = MODEL ? (FULL || ((uintptr_t)fmodel & 15u) == 0) : true;
 
 	// ---- phase 0: issue every load of the segment -----------------------
 	uint32_t firstc[CH];
@@ -489,10 +499,10 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 #pragma unroll
 	for (uint32_t c = 0; c < CH; c++) {
 		firstc[c] = sif * SEGN + c * AIRS_SEG + tid * AIRS_PT;
-		const bool full = firstc[c] + AIRS_PT <= n;
+		const bool full = FULL || firstc[c] + AIRS_PT <= n;
 		if (full && src_al) {
 			const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)firstc[c] * W);
-			if (a.dbg & 512u) { // ablation: no HBM reads (synthetic in-register data)
+			if (DBG(512u)) { // ablation: no HBM reads (synthetic in-register data)
 #pragma unroll
 				for (uint32_t q = 0; q < RW; q++)
 					raw[c][q] = make_uint4(0x40004000u + tid * 3u + q, 0x40104008u + c, 0x40204010u ^ tid,
@@ -509,7 +519,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			mraw[c][1] = p[1];
 		}
 		prevld[c] = 0u;
-		if (PRE == PRE_DIFF && lane == 0u && firstc[c] != 0u && firstc[c] <= n && !(a.dbg & 512u))
+		if (PRE == PRE_DIFF && lane == 0u && firstc[c] != 0u && firstc[c] <= n && !(DBG(512u)))
 			prevld[c] = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fsrc)[firstc[c] - 1u]
 					   : reinterpret_cast<const uint32_t *>(fsrc)[firstc[c] - 1u] & 0xFFFFu;
 	}
@@ -517,7 +527,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// zero both LDS chunk images while the loads are in flight
 	{
 		uint4 *L4 = reinterpret_cast<uint4 *>(L_dyn);
-		for (uint32_t i = tid; i < ((a.dbg & 4096u) ? 0u : 2u * IMGW / 4u); i += AIRS_WG)
+		for (uint32_t i = tid; i < ((DBG(4096u)) ? 0u : 2u * IMGW / 4u); i += AIRS_WG)
 			L4[i] = make_uint4(0u, 0u, 0u, 0u);
 	}
 
@@ -539,7 +549,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 #pragma unroll
 	for (uint32_t c = 0; c < CH; c++) {
 		const uint32_t first = firstc[c];
-		nv[c] = first >= n ? 0u : min(n - first, (uint32_t)AIRS_PT);
+		nv[c] = FULL ? (uint32_t)AIRS_PT : first >= n ? 0u : min(n - first, (uint32_t)AIRS_PT);
 		uint32_t w[AIRS_PT / 2]; // sample pairs (x[2j] | x[2j+1] << 16)
 		if (nv[c] == AIRS_PT && src_al) {
 			if (W == 2) {
@@ -605,10 +615,10 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				u = unpk(pk(w[j]) - pk(pm[j]));
 			else
 				u = w[j];
-			mp[c][j] = (a.dbg & 8192u) ? w[j] : (ENC == ENC_RAW ? u : zigzag_pk(u));
+			mp[c][j] = (DBG(8192u)) ? w[j] : (ENC == ENC_RAW ? u : zigzag_pk(u));
 		}
 		uint32_t t = 0u;
-		if (a.dbg & 64u) {
+		if (DBG(64u)) {
 			t = AIRS_PT * (cd.k + 1u) + (mp[c][0] & 7u);
 		} else if (fastk && nv[c] == AIRS_PT) {
 			u16x2 acc = (u16x2)(0);
@@ -649,7 +659,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			asm volatile("" : "+v"(mp[c][i]));
 	}
 
-	if (a.dbg & 32768u) { // ablation: stop after phase 1
+	if (DBG(32768u)) { // ablation: stop after phase 1
 		if (T[0] == 0x12345u && tid == 999u)
 			a.status[0] = mp[0][0] + mp[CH - 1][1];
 		return;
@@ -696,7 +706,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
 			gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
 		}
-		if (LBC == 0 && !is_first && !(a.dbg & 2u)) {
+		if (LBC == 0 && !is_first && !(DBG(2u))) {
 			// the first round's windows, newest first: with ~64 segments of a
 			// frame in flight the nearest inclusive prefix is often past 64
 #pragma unroll
@@ -709,7 +719,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				tv0 = gran_load(&a.tail[gseg - 1u]);
 		}
 	}
-	if (!is_last && wid == AIRS_WG / 64 - 1 && !(a.dbg & 8u)) {
+	if (!is_last && wid == AIRS_WG / 64 - 1 && !(DBG(8u))) {
 		// lane 255 holds >= 16 bits of the last chunk; lane 254 supplies the rest
 		uint64_t acc = 0u;
 		if (fastk && nv[CH - 1] == AIRS_PT) {
@@ -772,7 +782,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		// four words per thread: one 16-byte LDS read + its left neighbour, one
 		// 16-byte buffer store (the image is 16-byte aligned, j a multiple of 4)
 		const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)Lx);
-		const uint32_t nquad = (a.dbg & 2048u) ? 0u : (nfull >> 2);
+		const uint32_t nquad = (DBG(2048u)) ? 0u : (nfull >> 2);
 		for (uint32_t p = tid; p < nquad; p += AIRS_WG) {
 			const uint32_t j = 4u * p;
 			const u32x4 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + j);
@@ -782,18 +792,18 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			o.y = bswap32(__builtin_amdgcn_alignbit(w.x, w.y, r));
 			o.z = bswap32(__builtin_amdgcn_alignbit(w.y, w.z, r));
 			o.w = bswap32(__builtin_amdgcn_alignbit(w.z, w.w, r));
-			if (!(a.dbg & 1024u)) // ablation: no HBM writes
+			if (!(DBG(1024u))) // ablation: no HBM writes
 				__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
 		}
 		// the last nfull % 4 words: one each for the threads next in turn
 		// (thread 0 when one of them is word 0, the only word that needs
 		// predx, which lives in lane 0 of wave 0)
 		const uint32_t rr = (tid - nquad) & (AIRS_WG - 1u);
-		if (rr < (nfull & 3u) && !(a.dbg & 2048u)) {
+		if (rr < (nfull & 3u) && !(DBG(2048u))) {
 			const uint32_t j = 4u * nquad + rr;
 			const uint32_t hi = j ? Ll[j - 1u] : predx;
 			const uint32_t v = __builtin_amdgcn_alignbit(hi, Ll[j], r);
-			if (!(a.dbg & 1024u))
+			if (!(DBG(1024u)))
 				__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
 		}
 		if (finalx && nfull == J && tid == 0) {
@@ -825,11 +835,11 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			// image c&1 was last read by chunk c-2's stores (before the barrier
 			// that ended chunk c-1's packing): clear what it used
 			const uint32_t nw = (max(tot_m2, tot[0]) + 31u) >> 5;
-			for (uint32_t i = tid; i <= ((a.dbg & 4096u) ? 0u : nw); i += AIRS_WG)
+			for (uint32_t i = tid; i <= ((DBG(4096u)) ? 0u : nw); i += AIRS_WG)
 				Lc[i] = 0u;
 			__syncthreads();
 		}
-		if (LBC == 1 && c == 1u && wid == 0 && !is_first && !(a.dbg & 2u)) {
+		if (LBC == 1 && c == 1u && wid == 0 && !is_first && !(DBG(2u))) {
 #pragma unroll
 			for (int w = 0; w < LB_WIN; w++) {
 				const int64_t idx = (int64_t)gseg - 1 - 64 * w - (int64_t)lane;
@@ -843,7 +853,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		{
 			Packer pk1;
 			pk1.init(Lc, excl[0]);
-			if (a.dbg & 32u) {
+			if (DBG(32u)) {
 			} else if (fastk && nv[0] == AIRS_PT) {
 				// table-driven: byte offsets 8*min(q, 17) of both samples of a
 				// pair come from three packed ops; codeword = m + T'[q']
@@ -865,19 +875,32 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 							te[2 * jj + h] = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
 					}
 					// both codewords of a pair go in one put when they fit in 32
-					// bits (almost always); a longer pair takes two
+					// bits (almost always).  The test is made once per batch for
+					// the whole wave (one ballot, a uniform branch): if any lane
+					// has a longer pair, the whole batch takes two puts per pair.
+					uint32_t mxl = 0u;
+#pragma unroll
+					for (uint32_t i = 0; i < AIRS_PT / 2; i += 2)
+						mxl = max(mxl, te[i].y + te[i + 1].y);
+					if (__ballot(mxl > 32u) == 0ull) {
+#pragma unroll
+						for (uint32_t i = 0; i < AIRS_PT / 2; i += 2) {
+							const uint32_t j = hb * (AIRS_PT / 2) + i;
+							const uint32_t cwa = (mp[0][j >> 1] & 0xFFFFu) + te[i].x;
+							const uint32_t cwb = (mp[0][j >> 1] >> 16) + te[i + 1].x;
+							pk1.put((cwa << te[i + 1].y) | cwb, te[i].y + te[i + 1].y);
+						}
+					} else {
+#pragma unroll
+						for (uint32_t i = 0; i < AIRS_PT / 2; i += 2) {
+							const uint32_t j = hb * (AIRS_PT / 2) + i;
+							pk1.put((mp[0][j >> 1] & 0xFFFFu) + te[i].x, te[i].y);
+							pk1.put((mp[0][j >> 1] >> 16) + te[i + 1].x, te[i + 1].y);
+						}
+					}
 #pragma unroll
 					for (uint32_t i = 0; i < AIRS_PT / 2; i += 2) {
 						const uint32_t j = hb * (AIRS_PT / 2) + i;
-						const uint32_t cwa = (mp[0][j >> 1] & 0xFFFFu) + te[i].x;
-						const uint32_t cwb = (mp[0][j >> 1] >> 16) + te[i + 1].x;
-						const uint32_t lab = te[i].y + te[i + 1].y;
-						if (lab <= 32u) {
-							pk1.put((cwa << te[i + 1].y) | cwb, lab);
-						} else {
-							pk1.put(cwa, te[i].y);
-							pk1.put(cwb, te[i + 1].y);
-						}
 						ln[0][j] = te[i].y;
 						ln[0][j + 1] = te[i + 1].y;
 						if (NPIECE == 2) {
@@ -916,7 +939,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			// ---- decoupled look-back (wave 0), overlapped with the packing ----
 			if (wid == 0) {
 				uint32_t Pw = HDR_BITS;
-				if (a.dbg & 2u) {
+				if (DBG(2u)) {
 					Pw = HDR_BITS + sif * 37u; // ablation: no look-back (output garbage)
 				} else if (!is_first) {
 					// round 0 uses the granules fetched before packing; every
@@ -976,7 +999,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 					Pw = sum;
 					if (lane == 0)
 						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (Pw + A));
-					if ((a.dbg & 256u) && lane == 0) { // look-back statistics (debug)
+					if ((DBG(256u)) && lane == 0) { // look-back statistics (debug)
 						atomicAdd(a.ticket + 20, 1u);
 						atomicAdd(a.ticket + 21, lb_rounds);
 						atomicAdd(a.ticket + 22, spins);
@@ -984,7 +1007,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				}
 				if (lane == 0) {
 					uint32_t pred = 0u;
-					if (is_first || (a.dbg & 2u)) {
+					if (is_first || (DBG(2u))) {
 						// header bytes 20-21 (low half of the outlier field) share
 						// the first payload dword of a 22-byte header
 						pred = (EXT_HDR && ENC != ENC_RAW) ? (cd.outlier & 0xFFFFu) : 0u;
@@ -997,7 +1020,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 							}
 							__builtin_amdgcn_s_sleep(1);
 							tv = gran_load(&a.tail[gseg - 1u]);
-							if (a.dbg & 256u)
+							if (DBG(256u))
 								atomicAdd(a.ticket + 23, 1u);
 						}
 						pred = (uint32_t)tv;
@@ -1413,50 +1436,53 @@ static uint32_t ensure_granules(airs_dev_engine *e, size_t segs)
 }
 
 template <int W, int PRE, int ENC, bool RICE, int MODEL>
-static void launch_encode(const KArgs &k, uint32_t grid, hipStream_t s)
+static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t s)
 {
 	const size_t lds = (size_t)2u * (k.img_words + 4u) * 4u;
-	hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL>), dim3(grid), dim3(AIRS_WG), lds, s, k);
+	if (full)
+		hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true>), dim3(grid), dim3(AIRS_WG), lds, s, k);
+	else
+		hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, false>), dim3(grid), dim3(AIRS_WG), lds, s, k);
 }
 
 template <int W, int PRE, int MODEL>
-static void dispatch_enc(const KArgs &k, uint32_t enc, bool rice, uint32_t grid, hipStream_t s)
+static void dispatch_enc(const KArgs &k, uint32_t enc, bool rice, bool full, uint32_t grid, hipStream_t s)
 {
 	switch (enc) {
 	case ENC_RAW:
-		launch_encode<W, PRE, ENC_RAW, true, MODEL>(k, grid, s);
+		launch_encode<W, PRE, ENC_RAW, true, MODEL>(k, full, grid, s);
 		break;
 	case ENC_ZERO:
 		if (rice)
-			launch_encode<W, PRE, ENC_ZERO, true, MODEL>(k, grid, s);
+			launch_encode<W, PRE, ENC_ZERO, true, MODEL>(k, full, grid, s);
 		else
-			launch_encode<W, PRE, ENC_ZERO, false, MODEL>(k, grid, s);
+			launch_encode<W, PRE, ENC_ZERO, false, MODEL>(k, full, grid, s);
 		break;
 	default:
 		if (rice)
-			launch_encode<W, PRE, ENC_MULTI, true, MODEL>(k, grid, s);
+			launch_encode<W, PRE, ENC_MULTI, true, MODEL>(k, full, grid, s);
 		else
-			launch_encode<W, PRE, ENC_MULTI, false, MODEL>(k, grid, s);
+			launch_encode<W, PRE, ENC_MULTI, false, MODEL>(k, full, grid, s);
 		break;
 	}
 }
 
 template <int W>
-static void dispatch_pre(const KArgs &k, uint32_t pre, uint32_t enc, bool rice, uint32_t model_mode,
+static void dispatch_pre(const KArgs &k, uint32_t pre, uint32_t enc, bool rice, bool full, uint32_t model_mode,
 			 uint32_t grid, hipStream_t s)
 {
 	if (pre == PRE_MODEL) {
-		dispatch_enc<W, PRE_MODEL, AIRS_MODEL_UPDATE>(k, enc, rice, grid, s);
+		dispatch_enc<W, PRE_MODEL, AIRS_MODEL_UPDATE>(k, enc, rice, full, grid, s);
 	} else if (pre == PRE_DIFF) {
 		if (model_mode == AIRS_MODEL_STORE)
-			dispatch_enc<W, PRE_DIFF, AIRS_MODEL_STORE>(k, enc, rice, grid, s);
+			dispatch_enc<W, PRE_DIFF, AIRS_MODEL_STORE>(k, enc, rice, full, grid, s);
 		else
-			dispatch_enc<W, PRE_DIFF, AIRS_MODEL_NONE>(k, enc, rice, grid, s);
+			dispatch_enc<W, PRE_DIFF, AIRS_MODEL_NONE>(k, enc, rice, full, grid, s);
 	} else {
 		if (model_mode == AIRS_MODEL_STORE)
-			dispatch_enc<W, PRE_NONE, AIRS_MODEL_STORE>(k, enc, rice, grid, s);
+			dispatch_enc<W, PRE_NONE, AIRS_MODEL_STORE>(k, enc, rice, full, grid, s);
 		else
-			dispatch_enc<W, PRE_NONE, AIRS_MODEL_NONE>(k, enc, rice, grid, s);
+			dispatch_enc<W, PRE_NONE, AIRS_MODEL_NONE>(k, enc, rice, full, grid, s);
 	}
 }
 
@@ -1553,10 +1579,17 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 		    (L->encoder_param && (L->encoder_param & (L->encoder_param - 1u)) == 0u);
 	if (L->preprocessing == PRE_MODEL && L->model_mode != AIRS_MODEL_UPDATE)
 		return ERRV(E_PARAMS_INVALID);
+	// whole segments and 16-byte aligned frames (and models): the FULL kernel
+	bool full = L->n % segn == 0u && ((uintptr_t)L->src & 15u) == 0u && (L->src_stride & 15u) == 0u;
+	if (L->model_mode != AIRS_MODEL_NONE)
+		full = full && (L->model_ptrs ? L->model_ptrs_al16 != 0u
+					      : ((uintptr_t)L->model & 15u) == 0u && (L->model_stride & 15u) == 0u);
 	if (L->sample_bytes == 2)
-		dispatch_pre<2>(k, L->preprocessing, L->encoder_type, rice, L->model_mode, (uint32_t)segs, e->stream);
+		dispatch_pre<2>(k, L->preprocessing, L->encoder_type, rice, full, L->model_mode, (uint32_t)segs,
+				e->stream);
 	else
-		dispatch_pre<4>(k, L->preprocessing, L->encoder_type, rice, L->model_mode, (uint32_t)segs, e->stream);
+		dispatch_pre<4>(k, L->preprocessing, L->encoder_type, rice, full, L->model_mode, (uint32_t)segs,
+				e->stream);
 	HIPCHECK(hipGetLastError());
 	if (k.dbg & 4u)
 		e->ticket_base += (uint32_t)segs;

@@ -1,13 +1,17 @@
-# A/B: build the committed encode.hip as exp/base and the working tree as exp/new,
-# then time both (kbench) on the GPU box.  usage: bash scripts/ab.sh  (run locally, then gpurun scripts/gpu_exp.sh)
+# A/B: build the library of a git revision (default HEAD) as exp/base and the
+# working tree as exp/new, then time both on the GPU box with
+#   VARIANTS="base new" gpurun ... bash scripts/gpu_exp.sh
+# usage: bash scripts/ab.sh [REV]
 set -e
-rm -rf exp/base exp/new
-mkdir -p exp/base
-git show HEAD:airs-compression_amd/csrc/encode.hip > exp/base/encode_head.hip
-cp exp/base/encode_head.hip airs-compression_amd/csrc/.encode_head_tmp.hip
-bash scripts/build_exp.sh new ""
-(cd airs-compression_amd && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc \
-   -c csrc/.encode_head_tmp.hip -o ../exp/base/encode.o && \
- /opt/rocm/bin/hipcc -shared -Wl,-Bsymbolic -Wl,--no-undefined ../exp/base/encode.o build/cmp_host.o -o ../exp/base/libairscmp.so)
-rm -f airs-compression_amd/csrc/.encode_head_tmp.hip exp/base/encode.o exp/base/encode_head.hip
-ls exp/*/libairscmp.so
+REV=${1:-HEAD}
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+rm -rf "$ROOT/exp/base" "$ROOT/exp/new" /tmp/airs_ab
+mkdir -p "$ROOT/exp/base" "$ROOT/exp/new"
+git -C "$ROOT" worktree remove --force /tmp/airs_ab 2>/dev/null || true
+git -C "$ROOT" worktree add --detach /tmp/airs_ab "$REV" >/dev/null
+make -s -j8 -C /tmp/airs_ab/airs-compression_amd >/dev/null
+cp /tmp/airs_ab/airs-compression_amd/lib/libairscmp.so "$ROOT/exp/base/"
+git -C "$ROOT" worktree remove --force /tmp/airs_ab
+make -s -j8 -C "$ROOT/airs-compression_amd" >/dev/null
+cp "$ROOT/airs-compression_amd/lib/libairscmp.so" "$ROOT/exp/new/"
+ls -la "$ROOT"/exp/*/libairscmp.so
