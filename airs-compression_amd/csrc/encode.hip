@@ -1439,10 +1439,21 @@ template <int W, int PRE, int ENC, bool RICE, int MODEL>
 static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t s)
 {
 	const size_t lds = (size_t)2u * (k.img_words + 4u) * 4u;
+#ifdef AIRS_EXP_ONLY
+	// experiment builds: only the benchmark kernels (u16/i16, DIFF, ZERO, Rice, FULL)
+	if constexpr (!(W == 2 && PRE == PRE_DIFF && ENC == ENC_ZERO && RICE && MODEL == 0)) {
+		return;
+	} else {
+		if (full)
+			hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true>), dim3(grid), dim3(AIRS_WG), lds, s, k);
+		return;
+	}
+#else
 	if (full)
 		hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true>), dim3(grid), dim3(AIRS_WG), lds, s, k);
 	else
 		hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, false>), dim3(grid), dim3(AIRS_WG), lds, s, k);
+#endif
 }
 
 template <int W, int PRE, int MODEL>
