@@ -92,7 +92,7 @@ struct KArgs {
 	uint32_t ticket_base, epoch;
 	uint32_t img_words; // LDS image size: AIRS_SEG * (longest codeword) / 32 + 4, multiple of 4
 	uint32_t dbg; // ablation switches (AIRS_DBG env, benchmarking only; 0 in production)
-	uint64_t *dbgts; // AIRS_DBG bit 65536 (ablation builds): per-segment timestamps
+	uint64_t *dbgts; // AIRS_DBG bit 65536 (ablation builds): per-segment timeline
 };
 
 // ---------------------------------------------------------------------
@@ -406,7 +406,9 @@ __device__ __forceinline__ uint32_t gt16_mask(uint32_t q)
 	return (uint32_t)((int32_t)(16u - q) >> 31);
 }
 
-// debug timeline (ablation builds, AIRS_DBG bit 65536): realtime clock (100 MHz)
+// Debug timeline (ablation builds, AIRS_DBG bit 65536): per segment, 8
+// slots of the realtime clock (100 MHz): 0 start, 1 aggregate published,
+// 2 look-back done; slot 7 = HW_ID << 32 | XCC_ID.  scripts/ts_analyze.py.
 __device__ __forceinline__ void dbg_stamp(const KArgs &a, uint32_t gseg, uint32_t slot)
 {
 	if (DBG(65536u) && a.dbgts && threadIdx.x == 0) {
@@ -1141,499 +1143,6 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 }
 
 // ---------------------------------------------------------------------
-// Lean Rice kernel: the hot path of the BASELINE configs (u16/i16 or
-// i16-in-i32 input, NONE or DIFF, GOLOMB_ZERO with g = 2^k and k <= 11, no
-// model, whole 16-byte aligned segments).  Same algorithm as encode_kernel
-// (reference cmp.c:296-312 per sample), organised to keep waves busy:
-//
-//   * one LDS image holds the whole segment's bit stream (sized for k + 5
-//     bits per sample, not the worst case), so all chunks are packed before
-//     anything is stored and the look-back, issued right after the segment
-//     total is published, is only evaluated once all packing is done;
-//   * three barriers per segment (scan, packed, look-back) instead of three
-//     per chunk; one store pass over the image;
-//   * a segment whose stream exceeds the image (very noisy data) is packed
-//     and stored in windows of whole units (one wave's share of one chunk, in
-//     stream order), so the output is the same for any input.
-// ---------------------------------------------------------------------
-#ifndef AIRS_CAP_SLACK
-#define AIRS_CAP_SLACK 5
-#endif
-
-#ifndef AIRS_LEAN_CH
-#define AIRS_LEAN_CH 4
-#endif
-__host__ __device__ constexpr uint32_t rice_chunks(int W)
-{
-	return W == 2 ? AIRS_LEAN_CH : 2u;
-}
-
-// image words (excluding the 4 guard words in front): (k + slack) bits per
-// sample of the segment, at least two units' worth (a unit is 1024 samples of
-// at most k + 17 bits), plus spare words for the packer's flush; multiple of 4
-__host__ __device__ inline uint32_t rice_img_words(int W, uint32_t k)
-{
-	const uint32_t segn = rice_chunks(W) * AIRS_SEG;
-	uint32_t bits = segn * (k + AIRS_CAP_SLACK);
-	const uint32_t unit2 = 2u * 1024u * (k + 17u);
-	bits = bits > unit2 ? bits : unit2;
-	return ((bits + 31u) / 32u + 8u + 3u) & ~3u;
-}
-
-// Store bits [0, totx) of an LDS image (bit 0 = MSB of word 0) at frame bit
-// Pc: funnel-shift by Pc mod 32 (v_alignbit), byte-swap, write whole words
-// through the frame's buffer descriptor (its range, the capacity rounded down
-// to whole words, drops exactly the words that do not fit).  predx holds the
-// 32 stream bits before Pc (they complete the first word).  finalx: also
-// write the zero-padded last bytes (reference bitstream_flush).
-__device__ __forceinline__ void store_image(const uint32_t *Lx, uint32_t Pc, uint32_t totx, uint32_t predx,
-					    bool finalx, __amdgpu_buffer_rsrc_t rsrc, uint8_t *fdst, uint32_t cap,
-					    uint32_t tid)
-{
-	if (!totx)
-		return;
-	const uint32_t r = Pc & 31u, g0 = Pc >> 5;
-	const uint32_t endbit = Pc + totx;
-	const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
-	const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
-	const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)Lx);
-	const uint32_t nquad = nfull >> 2;
-	for (uint32_t p = tid; p < nquad; p += AIRS_WG) {
-		const uint32_t j = 4u * p;
-		const u32x4 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + j);
-		const uint32_t hi = j ? Ll[j - 1u] : predx;
-		u32x4 o;
-		o.x = bswap32(__builtin_amdgcn_alignbit(hi, w.x, r));
-		o.y = bswap32(__builtin_amdgcn_alignbit(w.x, w.y, r));
-		o.z = bswap32(__builtin_amdgcn_alignbit(w.y, w.z, r));
-		o.w = bswap32(__builtin_amdgcn_alignbit(w.z, w.w, r));
-		__builtin_amdgcn_raw_buffer_store_b128(o, rsrc, (int)(4u * (g0 + j)), 0, 0);
-	}
-	const uint32_t rr = (tid - nquad) & (AIRS_WG - 1u);
-	if (rr < (nfull & 3u)) {
-		const uint32_t j = 4u * nquad + rr;
-		const uint32_t hi = j ? Ll[j - 1u] : predx;
-		__builtin_amdgcn_raw_buffer_store_b32(bswap32(__builtin_amdgcn_alignbit(hi, Ll[j], r)), rsrc,
-						      (int)(4u * (g0 + j)), 0, 0);
-	}
-	if (finalx && nfull == J && tid == 0) {
-		const uint32_t hi = J ? Lx[J - 1u] : predx;
-		const uint32_t v = __builtin_amdgcn_alignbit(hi, Lx[J], r);
-		const uint32_t gw = g0 + J;
-		const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
-		for (uint32_t b = 0; b < nbytes; b++)
-			if (4u * gw + b < cap)
-				fdst[4u * gw + b] = (uint8_t)(v >> (24u - 8u * b));
-	}
-}
-
-// Decoupled look-back (wave 0): sum the predecessor aggregates of this frame
-// back to the nearest inclusive prefix.  gv holds the first round's
-// windows of 64 granules (newest first), fetched earlier.  Returns the frame
-// bit offset of this segment; bounded spins (fault word on give-up).
-template <int LBW>
-__device__ __forceinline__ uint32_t look_back(const KArgs &a, uint32_t gseg, uint32_t first_seg, uint32_t lane,
-					      uint64_t (&gv)[LBW])
-{
-	uint32_t sum = 0u, spins = 0u, rounds = 0u;
-	int64_t j = (int64_t)gseg - 1;
-	bool done = false;
-	while (!done) {
-		rounds++;
-		bool retry = false;
-#pragma unroll
-		for (int w = 0; w < LBW; w++) {
-			if (done || retry)
-				break;
-			const int64_t idx = j - 64 * w - (int64_t)lane;
-			const bool inr = idx >= (int64_t)first_seg;
-			const uint32_t tag = (uint32_t)(gv[w] >> 32);
-			const bool valid = inr && (tag >> 1) == a.epoch;
-			const bool incl = valid && (tag & 1u);
-			const uint64_t incl_m = __ballot(incl);
-			const uint64_t bad_m = __ballot(inr && !valid);
-			const uint32_t fi = incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
-			const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
-			if (bad_m & need) {
-				j -= 64 * w; // a needed predecessor has not published: re-poll from here
-				retry = true;
-				break;
-			}
-			sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv[w] : 0u);
-			if (incl_m)
-				done = true;
-		}
-		if (done)
-			break;
-		if (retry) {
-			if (++spins > AIRS_SPIN_LIMIT) {
-				if (lane == 0)
-					atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-				break;
-			}
-			__builtin_amdgcn_s_sleep(1);
-		} else {
-			j -= 64 * LBW;
-		}
-#pragma unroll
-		for (int w = 0; w < LBW; w++) {
-			const int64_t idx = j - 64 * w - (int64_t)lane;
-			gv[w] = idx >= (int64_t)first_seg ? gran_load(&a.agg[idx]) : 0ull;
-		}
-	}
-	if (DBG(256u) && lane == 0) { // look-back statistics (debug)
-		atomicAdd(a.ticket + 20, 1u);
-		atomicAdd(a.ticket + 21, rounds);
-		atomicAdd(a.ticket + 22, spins);
-	}
-	return sum;
-}
-
-#ifndef AIRS_LEAN_WPE
-#define AIRS_LEAN_WPE 5
-#endif
-template <int W, int PRE>
-__global__ __launch_bounds__(AIRS_WG) __attribute__((amdgpu_waves_per_eu(AIRS_LEAN_WPE, 8))) void rice_kernel(KArgs a)
-{
-	constexpr uint32_t CH = rice_chunks(W);
-	constexpr uint32_t NWV = AIRS_WG / 64;
-	constexpr uint32_t NU = CH * NWV; // units (chunk, wave) in stream order
-	constexpr uint32_t SEGN = CH * AIRS_SEG;
-	constexpr uint32_t RW = W == 2 ? 2u : 4u;
-	constexpr uint32_t HDR_BITS = 176u; // NONE/DIFF with GOLOMB_ZERO: 22-byte header
-	constexpr int LBW = 2;              // look-back windows of 64 granules per round
-#ifndef AIRS_LEAN_LBC
-#define AIRS_LEAN_LBC 1
-#endif
-	// look-back evaluated after this chunk's packing (its first round is
-	// fetched one chunk earlier)
-	constexpr uint32_t LBC = CH > AIRS_LEAN_LBC ? AIRS_LEAN_LBC : CH - 1u;
-	extern __shared__ __attribute__((aligned(16))) uint32_t L_dyn[]; // 4 guard words + image
-	__shared__ uint32_t s_wsum[CH][NWV];
-	__shared__ uint32_t s_misc[4];
-	__shared__ __attribute__((aligned(16))) uint2 s_rice[20];
-
-	const uint32_t tid = threadIdx.x, lane = tid & 63u;
-	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-	const uint32_t seg = blockIdx.x;
-	// frame-interleaved dispatch (see encode_kernel)
-	const uint32_t nfr = a.num_segs / a.segs_per_frame;
-	const uint32_t sif = seg / nfr;
-	const uint32_t lf = seg - sif * nfr;
-	const uint32_t gseg = lf * a.segs_per_frame + sif;
-	const uint32_t frame =
-		__builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
-	const bool is_first = sif == 0u;
-	const bool is_last = sif + 1u == a.segs_per_frame;
-	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
-	uint32_t *img = L_dyn + 4u;
-	dbg_stamp(a, gseg, 0);
-
-	// ---- phase 0: issue every load of the segment ----------------------
-	uint4 raw[CH][RW];
-	uint32_t prevld[CH];
-#pragma unroll
-	for (uint32_t c = 0; c < CH; c++) {
-		const uint32_t first = sif * SEGN + c * AIRS_SEG + tid * AIRS_PT;
-		const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)first * W);
-#pragma unroll
-		for (uint32_t q = 0; q < RW; q++)
-			raw[c][q] = p[q];
-		prevld[c] = 0u;
-		if (PRE == PRE_DIFF && lane == 0u && first != 0u)
-			prevld[c] = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fsrc)[first - 1u]
-					   : reinterpret_cast<const uint32_t *>(fsrc)[first - 1u] & 0xFFFFu;
-	}
-	{ // zero guard + image while the loads are in flight
-		uint4 *L4 = reinterpret_cast<uint4 *>(L_dyn);
-		for (uint32_t i = tid; i < (a.img_words + 4u) / 4u; i += AIRS_WG)
-			L4[i] = make_uint4(0u, 0u, 0u, 0u);
-	}
-	const uint32_t k = __builtin_amdgcn_readfirstlane(31u - (uint32_t)__clz((int)a.g));
-	const uint32_t kmask = (1u << k) - 1u;
-	if (tid < 18u)
-		s_rice[tid] = rice_table_entry(tid, k);
-
-	// ---- phase 1: residuals, ZigZag, code lengths (packed 16-bit) -------
-	uint32_t mp[CH][AIRS_PT / 2], T[CH];
-#pragma unroll
-	for (uint32_t c = 0; c < CH; c++) {
-		uint32_t w[AIRS_PT / 2];
-		if (W == 2) {
-			const uint32_t w8[8] = {raw[c][0].x, raw[c][0].y, raw[c][0].z, raw[c][0].w,
-						raw[c][1].x, raw[c][1].y, raw[c][1].z, raw[c][1].w};
-#pragma unroll
-			for (int j = 0; j < 8; j++)
-				w[j] = w8[j];
-		} else {
-#pragma unroll
-			for (uint32_t q = 0; q < 4; q++) {
-				w[2 * q] = __builtin_amdgcn_perm(raw[c][q].y, raw[c][q].x, 0x05040100u);
-				w[2 * q + 1] = __builtin_amdgcn_perm(raw[c][q].w, raw[c][q].z, 0x05040100u);
-			}
-		}
-		uint32_t wprev = 0u;
-		if (PRE == PRE_DIFF) {
-			wprev = __shfl_up(w[AIRS_PT / 2 - 1], 1, 64);
-			if (lane == 0u)
-				wprev = prevld[c] << 16;
-		}
-		u16x2 acc = (u16x2)(0);
-#pragma unroll
-		for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
-			uint32_t u = w[j];
-			if (PRE == PRE_DIFF)
-				u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
-			mp[c][j] = zigzag_pk(u);
-			acc += pk(rice_pair(mp[c][j], k, kmask).lq);
-		}
-		T[c] = AIRS_PT * (k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
-#pragma unroll
-		for (uint32_t i = 0; i < AIRS_PT / 2; i++)
-			asm volatile("" : "+v"(mp[c][i]));
-	}
-
-	// ---- scans: lane offsets inside each chunk, unit totals -------------
-	uint32_t inc[CH];
-#pragma unroll
-	for (uint32_t c = 0; c < CH; c++) {
-		inc[c] = wave_incl_scan(T[c]);
-		if (lane == 63u)
-			s_wsum[c][wid] = inc[c];
-	}
-	__syncthreads(); // B1: unit totals, table, zeroed image
-	// ustart[u]: segment bit offset of unit u (block-uniform)
-	uint32_t ustart[NU + 1];
-	ustart[0] = 0u;
-#pragma unroll
-	for (uint32_t u = 0; u < NU; u++)
-		ustart[u + 1] = ustart[u] + __builtin_amdgcn_readfirstlane(s_wsum[u / NWV][u % NWV]);
-	const uint32_t A = ustart[NU];
-	uint32_t lofs[CH]; // this lane's segment bit offset in chunk c
-#pragma unroll
-	for (uint32_t c = 0; c < CH; c++) {
-		uint32_t us = 0u;
-#pragma unroll
-		for (uint32_t w = 0; w < NWV; w++)
-			us = w == wid ? ustart[c * NWV + w] : us;
-		lofs[c] = us + inc[c] - T[c];
-	}
-
-	// ---- publish the aggregate; first look-back round in flight ----------
-	const uint32_t first_seg = gseg - sif;
-	uint64_t gv[LBW];
-#pragma unroll
-	for (int w = 0; w < LBW; w++)
-		gv[w] = 0;
-	uint64_t tv0 = 0;
-	if (wid == 0) {
-		if (lane == 0) {
-			const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
-			gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
-		}
-		dbg_stamp(a, gseg, 1);
-	}
-	// ---- the segment's last 32 bits (wave NWV-1 rebuilds its last chunk) --
-	if (!is_last && wid == NWV - 1) {
-		const char *tab = reinterpret_cast<const char *>(s_rice);
-		uint64_t acc = 0u;
-#pragma unroll
-		for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
-			const u16x2 v = __builtin_elementwise_add_sat(pk(mp[CH - 1][j]), (u16x2)(1));
-			const u16x2 qa = __builtin_elementwise_min(v >> (u16x2)((unsigned short)k), (u16x2)(17)) << (u16x2)(3);
-#pragma unroll
-			for (uint32_t h = 0; h < 2; h++) {
-				const uint2 e = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
-				acc = (acc << e.y) | (half16(mp[CH - 1][j], h) + e.x);
-			}
-		}
-		const uint32_t lo = (uint32_t)acc;
-		const uint32_t lo_prev = __shfl_up(lo, 1, 64);
-		if (lane == 63u) {
-			const uint32_t tl = T[CH - 1];
-			const uint32_t t32 = tl >= 32u ? lo : ((lo_prev << tl) | (lo & ((1u << tl) - 1u)));
-			gran_store(&a.tail[gseg], ((uint64_t)a.epoch << 32) | t32);
-		}
-		if (DBG(65536u) && a.dbgts && lane == 63u) {
-			uint64_t t;
-			asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t));
-			a.dbgts[8u * gseg + 6u] = t;
-		}
-	}
-
-	uint8_t *fdst = a.dst + (uint64_t)frame * a.dst_stride;
-	const uint32_t cap = a.cap;
-	const __amdgpu_buffer_rsrc_t dst_rsrc = __builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(cap & ~3u), 0x00020000);
-	const uint32_t capbits = (a.img_words - 8u) * 32u;
-	const char *tab = reinterpret_cast<const char *>(s_rice);
-
-	// ---- windows of whole units (one window unless the stream is too long) --
-	uint32_t u0 = 0u, P = 0u, pred = 0u;
-	for (bool first_win = true;; first_win = false) {
-		uint32_t wb = 0u, u1 = u0 + 1u;
-#pragma unroll
-		for (uint32_t u = 0; u < NU; u++)
-			wb = u == u0 ? ustart[u] : wb;
-#pragma unroll
-		for (uint32_t u = 0; u < NU; u++)
-			u1 = (u >= u0 && ustart[u + 1] - wb <= capbits) ? u + 1u : u1;
-		uint32_t we = 0u;
-#pragma unroll
-		for (uint32_t u = 1; u <= NU; u++)
-			we = u == u1 ? ustart[u] : we;
-		// pack: codeword = m + T'[min(q, 17)], both codewords of a pair in one
-		// put when every lane's pair of the batch fits in 32 bits
-#pragma unroll
-		for (uint32_t c = 0; c < CH; c++) {
-			const uint32_t u = c * NWV + wid;
-			if (first_win && wid == 0 && c + 1u == LBC && !is_first) {
-				// first look-back round, issued one chunk before it is
-				// evaluated (an earlier fetch mostly sees stale granules)
-#pragma unroll
-				for (int w = 0; w < LBW; w++) {
-					const int64_t idx = (int64_t)gseg - 1 - 64 * w - (int64_t)lane;
-					if (idx >= (int64_t)first_seg)
-						gv[w] = gran_load(&a.agg[idx]);
-				}
-				if (lane == 0)
-					tv0 = gran_load(&a.tail[gseg - 1u]);
-			}
-			if (u >= u0 && u < u1) {
-			// opaque per window: keeps the compiler from hoisting the
-			// (loop-invariant) table lookups of every chunk out of the loop
-#pragma unroll
-			for (uint32_t i = 0; i < AIRS_PT / 2; i++)
-				asm volatile("" : "+v"(mp[c][i]));
-			Packer pk1;
-			pk1.init(img, lofs[c] - wb);
-#pragma unroll
-			for (uint32_t hb = 0; hb < 2; hb++) {
-				uint2 te[AIRS_PT / 2];
-#pragma unroll
-				for (uint32_t jj = 0; jj < AIRS_PT / 4; jj++) {
-					const uint32_t j = hb * (AIRS_PT / 4) + jj;
-					const u16x2 v = __builtin_elementwise_add_sat(pk(mp[c][j]), (u16x2)(1));
-					const u16x2 qa =
-						__builtin_elementwise_min(v >> (u16x2)((unsigned short)k), (u16x2)(17)) << (u16x2)(3);
-#pragma unroll
-					for (uint32_t h = 0; h < 2; h++)
-						te[2 * jj + h] = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
-				}
-				uint32_t mxl = 0u;
-#pragma unroll
-				for (uint32_t i = 0; i < AIRS_PT / 2; i += 2)
-					mxl = max(mxl, te[i].y + te[i + 1].y);
-				if (__ballot(mxl > 32u) == 0ull) {
-#pragma unroll
-					for (uint32_t i = 0; i < AIRS_PT / 2; i += 2) {
-						const uint32_t m2 = mp[c][hb * (AIRS_PT / 4) + i / 2];
-						const uint32_t cwa = (m2 & 0xFFFFu) + te[i].x;
-						const uint32_t cwb = (m2 >> 16) + te[i + 1].x;
-						pk1.put((cwa << te[i + 1].y) | cwb, te[i].y + te[i + 1].y);
-					}
-				} else {
-#pragma unroll
-					for (uint32_t i = 0; i < AIRS_PT / 2; i += 2) {
-						const uint32_t m2 = mp[c][hb * (AIRS_PT / 4) + i / 2];
-						pk1.put((m2 & 0xFFFFu) + te[i].x, te[i].y);
-						pk1.put((m2 >> 16) + te[i + 1].x, te[i + 1].y);
-					}
-				}
-			}
-			pk1.flush();
-			}
-			// ---- look-back (wave 0, first window, after its chunk-LBC unit):
-			// publishes the inclusive prefix early; the other waves keep packing
-			if (first_win && wid == 0 && c == LBC) {
-				uint32_t Pw = HDR_BITS;
-				if (!is_first) {
-					dbg_stamp(a, gseg, 3);
-					Pw = look_back<LBW>(a, gseg, first_seg, lane, gv);
-					if (lane == 0)
-						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (Pw + A));
-				}
-				dbg_stamp(a, gseg, 2);
-				if (lane == 0) {
-					uint32_t pr;
-					if (is_first) {
-						// header bytes 20-21 (low half of the outlier) share the
-						// first payload dword of the 22-byte header
-						pr = make_coder<ENC_ZERO>(a.g, 0u).outlier & 0xFFFFu;
-					} else {
-						uint64_t tv = tv0;
-						for (uint32_t spins = 0; (uint32_t)(tv >> 32) != a.epoch; spins++) {
-							if (spins > AIRS_SPIN_LIMIT) {
-								atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-								break;
-							}
-							__builtin_amdgcn_s_sleep(1);
-							tv = gran_load(&a.tail[gseg - 1u]);
-							if (DBG(256u))
-								atomicAdd(a.ticket + 23, 1u);
-						}
-						pr = (uint32_t)tv;
-					}
-					s_misc[1] = Pw;
-					s_misc[2] = pr;
-				}
-				dbg_stamp(a, gseg, 4);
-			}
-		}
-		__syncthreads(); // B2: window packed (and P, pred in s_misc)
-		if (first_win) {
-			P = __builtin_amdgcn_readfirstlane(s_misc[1]);
-			pred = __builtin_amdgcn_readfirstlane(s_misc[2]);
-		}
-		store_image(img, P + wb, we - wb, pred, is_last && u1 == NU, dst_rsrc, fdst, cap, tid);
-		if (u1 >= NU) {
-			dbg_stamp(a, gseg, 5);
-			break;
-		}
-		// next window: the 32 bits before it, then clear what this one used
-		{
-			const uint32_t s0 = we - wb - 32u, q = s0 >> 5, sh = s0 & 31u;
-			pred = __builtin_amdgcn_readfirstlane(sh ? (img[q] << sh) | (img[q + 1] >> (32u - sh)) : img[q]);
-		}
-		__syncthreads();
-		const uint32_t nw = (we - wb + 31u) / 32u + 2u;
-		for (uint32_t i = tid; i < nw; i += AIRS_WG)
-			img[i] = 0u;
-		__syncthreads();
-		u0 = u1;
-	}
-
-	// ---- frame epilogue: checksum, header, status ------------------------
-	if (is_last && tid == 0) {
-		const uint32_t n = a.n;
-		const uint32_t endbit = P + A;
-		const uint32_t payload_bytes = (endbit + 7u) >> 3;
-		const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
-		if (a.checksum) {
-			const uint32_t ck = a.checksums[frame];
-			for (uint32_t b = 0; b < 4u; b++)
-				if (payload_bytes + b < cap)
-					fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
-		}
-		const uint64_t id = a.ids ? a.ids[lf] : a.id_base + (uint64_t)lf * a.id_step;
-		uint32_t h[5];
-		header_words(h, size, 2u * n, id, a.seq, PRE, a.checksum ? 1u : 0u, ENC_ZERO, 0u, a.g,
-			     make_coder<ENC_ZERO>(a.g, 0u).outlier);
-#pragma unroll
-		for (uint32_t w = 0; w < 5u; w++)
-			if (4u * w + 4u <= cap)
-				*reinterpret_cast<uint32_t *>(fdst + 4u * w) = bswap32(h[w]);
-		uint32_t st = size;
-		if (size > cap)
-			st = ERRV(E_DST_TOO_SMALL);
-		else if (size > 0xFFFFFFu)
-			st = ERRV(E_HDR_CMP_SIZE_TOO_LARGE);
-		a.status[frame] = st;
-		if (a.needed)
-			a.needed[frame] = size;
-	}
-}
-
-// ---------------------------------------------------------------------
 // XXH32 per frame over big-endian 16-bit samples (reference header.c:137-163).
 // The four accumulators of a frame run in four lanes; each stripe is 8
 // samples = 16 bytes, lane q consumes bytes 4q..4q+3 of every stripe.
@@ -1862,7 +1371,7 @@ struct airs_dev_engine {
 	uint32_t epoch;
 	void *scratch[AIRS_NSLOT];
 	size_t scratch_cap[AIRS_NSLOT];
-	uint64_t *dbgts;      // debug timeline (AIRS_DBG bit 65536)
+	uint64_t *dbgts; // debug timeline (AIRS_DBG bit 65536)
 	size_t dbgts_n;
 };
 
@@ -1905,6 +1414,7 @@ extern "C" void airs_dev_engine_destroy(struct airs_dev_engine *e)
 	(void)hipFree(e->agg);
 	(void)hipFree(e->tail);
 	(void)hipFree(e->ticket);
+	(void)hipFree(e->dbgts);
 	for (int i = 0; i < AIRS_NSLOT; i++)
 		(void)hipFree(e->scratch[i]);
 	free(e);
@@ -2020,18 +1530,7 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 		return ERRV(E_PARAMS_INVALID);
 	if (L->encoder_type > ENC_MULTI || (L->sample_bytes != 2 && L->sample_bytes != 4))
 		return ERRV(E_PARAMS_INVALID);
-	const int W = L->sample_bytes == 4 ? 4 : 2;
-	const bool src_al16 = ((uintptr_t)L->src & 15u) == 0u && (L->src_stride & 15u) == 0u;
-	// the hot path (BASELINE configs 2-4) goes to the lean Rice kernel: whole
-	// aligned segments, GOLOMB_ZERO with one g = 2^k (k <= 11), no model
-	bool lean = L->encoder_type == ENC_ZERO && !L->frame_g && L->encoder_param &&
-		    (L->encoder_param & (L->encoder_param - 1u)) == 0u && L->encoder_param <= 2048u &&
-		    L->model_mode == AIRS_MODEL_NONE && (L->preprocessing == PRE_NONE || L->preprocessing == PRE_DIFF) &&
-		    src_al16 && L->n % (rice_chunks(W) * AIRS_SEG) == 0u;
-#ifdef AIRS_NO_LEAN
-	lean = false;
-#endif
-	const uint32_t segn = (lean ? rice_chunks(W) : seg_chunks(W, L->model_mode ? 1 : 0)) * AIRS_SEG;
+	const uint32_t segn = seg_chunks(L->sample_bytes == 4 ? 4 : 2, L->model_mode ? 1 : 0) * AIRS_SEG;
 	const uint32_t spf = (L->n + segn - 1) / segn;
 	const uint64_t segs = (uint64_t)spf * L->num_frames;
 	if (segs > 0x7FFFFFFFull)
@@ -2127,33 +1626,10 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	if (L->preprocessing == PRE_MODEL && L->model_mode != AIRS_MODEL_UPDATE)
 		return ERRV(E_PARAMS_INVALID);
 	// whole segments and 16-byte aligned frames (and models): the FULL kernel
-	bool full = L->n % segn == 0u && src_al16;
+	bool full = L->n % segn == 0u && ((uintptr_t)L->src & 15u) == 0u && (L->src_stride & 15u) == 0u;
 	if (L->model_mode != AIRS_MODEL_NONE)
 		full = full && (L->model_ptrs ? L->model_ptrs_al16 != 0u
 					      : ((uintptr_t)L->model & 15u) == 0u && (L->model_stride & 15u) == 0u);
-	if (lean) {
-		uint32_t kk = 0u;
-		while ((2u << kk) <= L->encoder_param)
-			kk++;
-		k.img_words = rice_img_words(L->sample_bytes == 4 ? 4 : 2, kk);
-		const size_t lds = (size_t)(k.img_words + 4u) * 4u;
-		const dim3 grid((uint32_t)segs), blk(AIRS_WG);
-		if (L->sample_bytes == 2) {
-			if (L->preprocessing == PRE_DIFF)
-				hipLaunchKernelGGL((rice_kernel<2, PRE_DIFF>), grid, blk, lds, e->stream, k);
-#ifndef AIRS_EXP_ONLY
-			else
-				hipLaunchKernelGGL((rice_kernel<2, PRE_NONE>), grid, blk, lds, e->stream, k);
-		} else {
-			if (L->preprocessing == PRE_DIFF)
-				hipLaunchKernelGGL((rice_kernel<4, PRE_DIFF>), grid, blk, lds, e->stream, k);
-			else
-				hipLaunchKernelGGL((rice_kernel<4, PRE_NONE>), grid, blk, lds, e->stream, k);
-#endif
-		}
-		HIPCHECK(hipGetLastError());
-		return 0;
-	}
 	if (L->sample_bytes == 2)
 		dispatch_pre<2>(k, L->preprocessing, L->encoder_type, rice, full, L->model_mode, (uint32_t)segs,
 				e->stream);
@@ -2290,13 +1766,13 @@ extern "C" uint32_t airs_dev_sync(struct airs_dev_engine *e)
 			const char *v = getenv("AIRS_DBG");
 			dbg = v ? atoi(v) : 0;
 		}
-		if (dbg & 65536) {
+		if (dbg & 65536) { // dump the debug timeline to $AIRS_DBGTS_PATH
 			const char *path = getenv("AIRS_DBGTS_PATH");
 			FILE *f = path ? fopen(path, "wb") : nullptr;
 			if (f && e->dbgts) {
 				uint64_t *h = (uint64_t *)malloc(e->dbgts_n * 8u);
-				HIPCHECK(hipMemcpy(h, e->dbgts, e->dbgts_n * 8u, hipMemcpyDeviceToHost));
-				fwrite(h, 8u, e->dbgts_n, f);
+				if (h && hipMemcpy(h, e->dbgts, e->dbgts_n * 8u, hipMemcpyDeviceToHost) == hipSuccess)
+					fwrite(h, 8u, e->dbgts_n, f);
 				free(h);
 			}
 			if (f)
