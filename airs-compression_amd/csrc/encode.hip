@@ -415,6 +415,11 @@ __device__ __forceinline__ void dbg_stamp(const KArgs &a, uint32_t gseg, uint32_
 		uint64_t t;
 		asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t));
 		a.dbgts[8u * gseg + slot] = t;
+		if (slot == 0 || slot == 2) { // shader clock counter next to the realtime stamps
+			uint64_t c;
+			asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(c));
+			a.dbgts[8u * gseg + (slot == 0 ? 5u : 6u)] = c;
+		}
 		if (slot == 0) {
 			uint32_t hw, xcc;
 			asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -440,9 +445,12 @@ __device__ __forceinline__ void dbg_stamp(const KArgs &a, uint32_t gseg, uint32_
 // codewords chunk by chunk into a double-buffered LDS image and stores them
 // once the look-back has produced the segment's frame bit offset.
 // ---------------------------------------------------------------------
+#ifndef AIRS_SEG_CH
+#define AIRS_SEG_CH 4
+#endif
 __host__ __device__ constexpr uint32_t seg_chunks(int W, int MODEL)
 {
-	return (W == 4 || MODEL) ? 2u : 4u;
+	return (W == 4 || MODEL) ? 2u : AIRS_SEG_CH;
 }
 
 template <int W, int PRE, int ENC, bool RICE, int MODEL, bool FULL>

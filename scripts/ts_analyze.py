@@ -26,3 +26,9 @@ print(f" pred agg after succ LB start: {np.mean(ag2[:, :-1] > lbs2[:, 1:]) * 100
       f"pred started after succ: {np.mean(st2[:, :-1] > st2[:, 1:]) * 100:.1f}%")
 d = lbd2[:, 1:] - lbd2[:, :-1]
 print(f" succ LB done - pred LB done: {R(d)}")
+# shader clock: slots 5/6 = s_memtime at start / look-back done (encode_kernel)
+c0, c1 = a[:, 5].astype(np.int64), a[:, 6].astype(np.int64)
+ok = (c0 > 0) & (c1 > c0) & (t[:, 2] > t[:, 0])
+if ok.any():
+    f = (c1 - c0)[ok] / ((t[:, 2] - t[:, 0])[ok] / 100.0)  # cycles per us
+    print(f" shader clock (s_memtime / realtime): median {np.median(f) / 1e3:.3f} GHz  p10 {np.percentile(f, 10) / 1e3:.3f}  p90 {np.percentile(f, 90) / 1e3:.3f}")
