@@ -400,6 +400,24 @@ __device__ __forceinline__ uint2 rice_table_entry(uint32_t q, uint32_t k)
 	return make_uint2(t, k + 1u + q);
 }
 
+// First look-back round's granule loads (wave 0, not the frame's first
+// segment): LB_WIN windows of 64 aggregates, newest first, and the
+// predecessor's tail.  Addresses are clamped into the frame instead of
+// predicated, so the loads need no exec-mask branch (a predicated load made
+// the compiler wait for it right away); the evaluation ignores the clamped
+// lanes.
+template <int LB_WIN>
+__device__ __forceinline__ void lb_prefetch(const KArgs &a, uint64_t (&gv)[LB_WIN], uint64_t &tv0, uint32_t gseg,
+					    uint32_t first_seg, uint32_t lane)
+{
+#pragma unroll
+	for (int w = 0; w < LB_WIN; w++) {
+		const int64_t idx = (int64_t)gseg - 1 - 64 * w - (int64_t)lane;
+		gv[w] = gran_load(&a.agg[idx >= (int64_t)first_seg ? idx : (int64_t)first_seg]);
+	}
+	tv0 = gran_load(&a.tail[gseg - 1u]);
+}
+
 // all-ones when q > 16 (q < 2^16)
 __device__ __forceinline__ uint32_t gt16_mask(uint32_t q)
 {
@@ -408,18 +426,14 @@ __device__ __forceinline__ uint32_t gt16_mask(uint32_t q)
 
 // Debug timeline (ablation builds, AIRS_DBG bit 65536): per segment, 8
 // slots of the realtime clock (100 MHz): 0 start, 1 aggregate published,
-// 2 look-back done; slot 7 = HW_ID << 32 | XCC_ID.  scripts/ts_analyze.py.
+// 2 look-back done, 3 look-back start, 4 segment done (wave 0); 5 look-back
+// rounds | retries << 32, 6 tail re-polls; slot 7 = HW_ID << 32 | XCC_ID.  scripts/ts_analyze.py.
 __device__ __forceinline__ void dbg_stamp(const KArgs &a, uint32_t gseg, uint32_t slot)
 {
 	if (DBG(65536u) && a.dbgts && threadIdx.x == 0) {
 		uint64_t t;
 		asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t));
 		a.dbgts[8u * gseg + slot] = t;
-		if (slot == 0 || slot == 2) { // shader clock counter next to the realtime stamps
-			uint64_t c;
-			asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(c));
-			a.dbgts[8u * gseg + (slot == 0 ? 5u : 6u)] = c;
-		}
 		if (slot == 0) {
 			uint32_t hw, xcc;
 			asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -452,6 +466,15 @@ __host__ __device__ constexpr uint32_t seg_chunks(int W, int MODEL)
 {
 	return (W == 4 || MODEL) ? 2u : AIRS_SEG_CH;
 }
+// LDS chunk images per workgroup: with three, the look-back is evaluated
+// after the third chunk's packing (chunks 0 and 1 are stored late)
+#ifndef AIRS_NIMG
+#define AIRS_NIMG 3
+#endif
+__host__ __device__ constexpr uint32_t seg_images(int W, int MODEL)
+{
+	return (seg_chunks(W, MODEL) >= 4u && !MODEL) ? AIRS_NIMG : 2u;
+}
 
 template <int W, int PRE, int ENC, bool RICE, int MODEL, bool FULL>
 __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
@@ -464,14 +487,12 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// ends, so they see the predecessors one chunk later than the aggregate
 	// publish (which an earlier poll mostly misses); chunk 0 is stored late.
 	// 0 with a model, whose chunk-0 update needs the bit offset first.
-#ifndef AIRS_LBC
-#define AIRS_LBC 1u
-#endif
-	constexpr uint32_t LBC = (MODEL || CH < 2) ? 0u : AIRS_LBC;
+	constexpr uint32_t NIMG = seg_images(W, MODEL);
+	constexpr uint32_t LBC = (MODEL || CH < 2) ? 0u : NIMG - 1u;
 	constexpr uint32_t RW = W == 2 ? 2u : 4u; // uint4 per lane per chunk
 	constexpr bool EXT_HDR = !(PRE == PRE_NONE && ENC == ENC_RAW);
 	constexpr uint32_t HDR_BITS = EXT_HDR ? 176u : 128u;
-	// two chunk images in dynamic LDS, a.img_words each (sized per launch from
+	// NIMG chunk images in dynamic LDS, a.img_words each (sized per launch from
 	// the longest codeword the pass can emit), each after a 4-word guard
 	extern __shared__ __attribute__((aligned(16))) uint32_t L_dyn[];
 	const uint32_t IMGW = a.img_words + 4u; // words per image incl. guard (multiple of 4)
@@ -555,7 +576,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// zero both LDS chunk images while the loads are in flight
 	{
 		uint4 *L4 = reinterpret_cast<uint4 *>(L_dyn);
-		for (uint32_t i = tid; i < ((DBG(4096u)) ? 0u : 2u * IMGW / 4u); i += AIRS_WG)
+		for (uint32_t i = tid; i < ((DBG(4096u)) ? 0u : NIMG * IMGW / 4u); i += AIRS_WG)
 			L4[i] = make_uint4(0u, 0u, 0u, 0u);
 	}
 
@@ -738,14 +759,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		if (LBC == 0 && !is_first && !(DBG(2u))) {
 			// the first round's windows, newest first: with ~64 segments of a
 			// frame in flight the nearest inclusive prefix is often past 64
-#pragma unroll
-			for (int w = 0; w < LB_WIN; w++) {
-				const int64_t idx = (int64_t)gseg - 1 - 64 * w - (int64_t)lane;
-				if (idx >= (int64_t)first_seg)
-					gv[w] = gran_load(&a.agg[idx]);
-			}
-			if (lane == 0)
-				tv0 = gran_load(&a.tail[gseg - 1u]);
+			lb_prefetch<LB_WIN>(a, gv, tv0, gseg, first_seg, lane);
 		}
 	}
 	if (!is_last && wid == AIRS_WG / 64 - 1 && !(DBG(8u))) {
@@ -850,33 +864,31 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// ---- phase 2: chunk by chunk: codewords -> LDS image -> HBM -----------
 	// rolled loop (keeps register pressure flat): the current chunk's state is
 	// always index 0 of mp/nmp/nv/excl/tot/base/firstc, rotated at the end
-	uint32_t tot_m2 = 0u; // total of chunk c-2 (its image is recycled now)
+	uint32_t tot_m3 = 0u; // totals of chunks c-3, c-2 (an image is recycled now), c-1
+	uint32_t tot_m2 = 0u;
 	uint32_t tot_m1 = 0u;
+	uint32_t pred_1 = 0u; // (tid 0) last 32 bits of chunk 0, kept for chunk 1's late store
 #ifndef AIRS_CHUNK_UNROLL
-#define AIRS_CHUNK_UNROLL 1
+#define AIRS_CHUNK_UNROLL 4
 #endif
 #pragma unroll AIRS_CHUNK_UNROLL
 	for (uint32_t c = 0; c < CH; c++) {
-		uint32_t *Lc = L_dyn + (c & 1u) * IMGW + 4u;
-		if (LBC == 1 && c == 2u)
+		uint32_t *Lc = L_dyn + (c % NIMG) * IMGW + 4u;
+		if (LBC >= 1 && c == LBC + 1u && c >= NIMG)
 			__syncthreads(); // chunk 0's image was stored (late) after the last barrier
-		if (c >= 2) {
-			// image c&1 was last read by chunk c-2's stores (before the barrier
-			// that ended chunk c-1's packing): clear what it used
-			const uint32_t nw = (max(tot_m2, tot[0]) + 31u) >> 5;
+		if (c >= NIMG) {
+			// image c%NIMG was last read by chunk c-NIMG's stores (before the
+			// barrier that ended chunk c-1's packing): clear what it used
+			const uint32_t nw = (max(NIMG == 2 ? tot_m2 : tot_m3, tot[0]) + 31u) >> 5;
 			for (uint32_t i = tid; i <= ((DBG(4096u)) ? 0u : nw); i += AIRS_WG)
 				Lc[i] = 0u;
 			__syncthreads();
 		}
-		if (LBC == 1 && c == 1u && wid == 0 && !is_first && !(DBG(2u))) {
-#pragma unroll
-			for (int w = 0; w < LB_WIN; w++) {
-				const int64_t idx = (int64_t)gseg - 1 - 64 * w - (int64_t)lane;
-				if (idx >= (int64_t)first_seg)
-					gv[w] = gran_load(&a.agg[idx]);
-			}
-			if (lane == 0)
-				tv0 = gran_load(&a.tail[gseg - 1u]);
+#ifndef AIRS_LBP
+#define AIRS_LBP LBC
+#endif
+		if (LBC >= 1 && c == (AIRS_LBP) && wid == 0 && !is_first && !(DBG(2u))) {
+			lb_prefetch<LB_WIN>(a, gv, tv0, gseg, first_seg, lane);
 		}
 		uint32_t ln[NPIECE][AIRS_PT]; // piece lengths (kept for the MODEL fail_bit check)
 		{
@@ -967,6 +979,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		if (c == LBC) {
 			// ---- decoupled look-back (wave 0), overlapped with the packing ----
 			if (wid == 0) {
+				dbg_stamp(a, gseg, 3);
 				uint32_t Pw = HDR_BITS;
 				if (DBG(2u)) {
 					Pw = HDR_BITS + sif * 37u; // ablation: no look-back (output garbage)
@@ -1028,6 +1041,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 					Pw = sum;
 					if (lane == 0)
 						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (Pw + A));
+					if ((DBG(65536u)) && a.dbgts && lane == 0)
+						a.dbgts[8u * gseg + 5u] = ((uint64_t)spins << 32) | lb_rounds;
 					if ((DBG(256u)) && lane == 0) { // look-back statistics (debug)
 						atomicAdd(a.ticket + 20, 1u);
 						atomicAdd(a.ticket + 21, lb_rounds);
@@ -1042,7 +1057,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 						pred = (EXT_HDR && ENC != ENC_RAW) ? (cd.outlier & 0xFFFFu) : 0u;
 					} else {
 						uint64_t tv = tv0;
-						for (uint32_t spins = 0; (uint32_t)(tv >> 32) != a.epoch; spins++) {
+						uint32_t spins = 0;
+						for (; (uint32_t)(tv >> 32) != a.epoch; spins++) {
 							if (spins > AIRS_SPIN_LIMIT) {
 								atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
 								break;
@@ -1052,6 +1068,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 							if (DBG(256u))
 								atomicAdd(a.ticket + 23, 1u);
 						}
+						if ((DBG(65536u)) && a.dbgts)
+							a.dbgts[8u * gseg + 6u] = spins;
 						pred = (uint32_t)tv;
 					}
 					s_misc[1] = Pw;
@@ -1066,6 +1084,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				pred_c = seg_pred;
 			else if (tot_first) // chunk 0 waited for the look-back: store it now
 				store_chunk(L_dyn + 4u, 0u, tot_first, seg_pred, is_last && last_ne == 0u);
+			if (LBC == 2) // so did chunk 1
+				store_chunk(L_dyn + IMGW + 4u, tot_first, tot_m1, pred_1, is_last && last_ne == 1u);
 		}
 
 		if (c >= LBC)
@@ -1098,8 +1118,11 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 						mpp[j] = (uint16_t)(nmp[0][j >> 1] >> (16u * (j & 1u)));
 			}
 		}
+		if (c == 0)
+			pred_1 = pred_next;
 		pred_c = pred_next;
 		// rotate the per-chunk state
+		tot_m3 = tot_m2;
 		tot_m2 = tot_m1;
 		tot_m1 = tot[0];
 #pragma unroll
@@ -1118,6 +1141,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		}
 	}
 
+	dbg_stamp(a, gseg, 4);
 	// ---- frame epilogue: checksum, header, status ------------------------
 	if (is_last && tid == 0) {
 		const uint32_t endbit = P + A;
@@ -1471,7 +1495,10 @@ static uint32_t ensure_granules(airs_dev_engine *e, size_t segs)
 template <int W, int PRE, int ENC, bool RICE, int MODEL>
 static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t s)
 {
-	const size_t lds = (size_t)2u * (k.img_words + 4u) * 4u;
+#ifndef AIRS_LDS_EXTRA
+#define AIRS_LDS_EXTRA 0
+#endif
+	const size_t lds = (size_t)seg_images(W, MODEL) * (k.img_words + 4u) * 4u + AIRS_LDS_EXTRA; // (extra: occupancy experiments)
 #ifdef AIRS_EXP_ONLY
 	// experiment builds: only the benchmark kernels (u16/i16, DIFF, ZERO, Rice, FULL)
 	if constexpr (!(W == 2 && PRE == PRE_DIFF && ENC == ENC_ZERO && RICE && MODEL == 0)) {
@@ -1603,6 +1630,9 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 			}
 			maxbits = kk + 17u < 32u ? kk + 17u : 32u;
 		}
+#ifdef AIRS_IMG_BITS // experiments only: images too small for the worst case
+		maxbits = AIRS_IMG_BITS;
+#endif
 		const uint32_t words = AIRS_SEG * maxbits / 32u + 4u;
 		k.img_words = (words + 3u) & ~3u;
 	}

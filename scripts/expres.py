@@ -1,8 +1,9 @@
-"""Summarise gpurun_out/exp.jsonl (written by scripts/gpu_exp.sh): variant workload median/min us."""
-import json, sys
+"""print gpurun_out/exp.jsonl as a table: variant workload us GB/s bitexact"""
+import json
 v = None
-for l in open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/exp.jsonl"):
-    d = json.loads(l)
+for line in open("gpurun_out/exp.jsonl"):
+    d = json.loads(line)
     if "variant" in d:
-        v = d["variant"]; continue
-    print(f'{v:8s} {d["workload"]:6s} dbg={d["dbg"]:>6s} median {d["median_ms"]*1000:7.2f} us  min {d["min_ms"]*1000:7.2f} us  exact={d.get("bitexact")}')
+        v = d["variant"]
+        continue
+    print(f"{v:8s} {d['workload']} {d['median_ms'] * 1000:7.1f} us {d['GBps']:8.1f} GB/s  bitexact={d['bitexact']}")

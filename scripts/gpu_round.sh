@@ -10,4 +10,4 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt 
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o pf -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/pf.log 2>&1 && \
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $O/pw -o pw -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/pw.log 2>&1 && \
 python3 scripts/traffic.py $O/pf/pf_results.db $O/pw/pw_results.db cfg2 $O/traffic_cfg2.json > $O/traffic.log 2>&1 && \
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
