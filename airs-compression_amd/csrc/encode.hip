@@ -330,23 +330,6 @@ __device__ __forceinline__ uint32_t zigzag_pk(uint32_t u)
 	return unpk((x << (u16x2)(1)) ^ __builtin_bit_cast(u16x2, __builtin_bit_cast(i16x2, x) >> (i16x2)(15)));
 }
 
-// Rice/ZERO pair terms: v = m + 1 saturated at 0xFFFF (exact for k <= 11,
-// where m = 0xFFFF escapes either way), q = v >> k, low = v & (2^k - 1)
-struct RicePair {
-	uint32_t q, low, lq; // packed; lq = min(q, 16)
-};
-
-__device__ __forceinline__ RicePair rice_pair(uint32_t m2, uint32_t k, uint32_t mask)
-{
-	const u16x2 v = __builtin_elementwise_add_sat(pk(m2), (u16x2)(1));
-	const u16x2 q = v >> (u16x2)((unsigned short)k);
-	RicePair r;
-	r.q = unpk(q);
-	r.low = unpk(v & (u16x2)((unsigned short)mask));
-	r.lq = unpk(__builtin_elementwise_min(q, (u16x2)(16)));
-	return r;
-}
-
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // Bit packer into an LDS image.  `nb` is a bit position in the LDS address
@@ -589,10 +572,15 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// packed ops, and for Rice/ZERO with k <= 11 the code lengths are summed
 	// with packed ops too (length = k + 1 + min((m + 1) >> k, 16)).
 	const bool fastk = ENC == ENC_ZERO && RICE && cd.k <= 11u;
-	const uint32_t kmask = (1u << cd.k) - 1u;
 	if (fastk && tid < 18u)
 		s_rice[tid] = rice_table_entry(tid, cd.k);
 	uint32_t mp[CH][AIRS_PT / 2]; // mapped values, two 16-bit per register
+	// Rice/ZERO fast path (AIRS_KEEP_Q): the code-table byte offsets
+	// 8 min(q, 17) of every pair, computed once in phase 1 next to the lengths
+#ifndef AIRS_KEEP_Q
+#define AIRS_KEEP_Q 1
+#endif
+	uint32_t mq[AIRS_KEEP_Q ? CH : 1][AIRS_PT / 2];
 	uint32_t nmp[MODEL ? CH : 1][AIRS_PT / 2]; // new model values (MODEL)
 	uint32_t T[CH], nv[CH];
 #pragma unroll
@@ -672,8 +660,13 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		} else if (fastk && nv[c] == AIRS_PT) {
 			u16x2 acc = (u16x2)(0);
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT / 2; j++)
-				acc += pk(rice_pair(mp[c][j], cd.k, kmask).lq);
+			for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+				const u16x2 v = __builtin_elementwise_add_sat(pk(mp[c][j]), (u16x2)(1));
+				const u16x2 q = v >> (u16x2)((unsigned short)cd.k);
+				acc += __builtin_elementwise_min(q, (u16x2)(16));
+				if (AIRS_KEEP_Q)
+					mq[AIRS_KEEP_Q ? c : 0][j] = unpk(__builtin_elementwise_min(q, (u16x2)(17)) << (u16x2)(3));
+			}
 			t = AIRS_PT * (cd.k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
 		} else {
 #pragma unroll
@@ -706,6 +699,11 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 #pragma unroll
 		for (uint32_t i = 0; i < AIRS_PT / 2; i++)
 			asm volatile("" : "+v"(mp[c][i]));
+		if (AIRS_KEEP_Q) {
+#pragma unroll
+			for (uint32_t i = 0; i < AIRS_PT / 2; i++)
+				asm volatile("" : "+v"(mq[AIRS_KEEP_Q ? c : 0][i]));
+		}
 	}
 
 	if (DBG(32768u)) { // ablation: stop after phase 1
@@ -907,10 +905,14 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 #pragma unroll
 					for (uint32_t jj = 0; jj < AIRS_PT / 4; jj++) {
 						const uint32_t j = hb * (AIRS_PT / 4) + jj;
-						const u16x2 v = __builtin_elementwise_add_sat(pk(mp[0][j]), (u16x2)(1));
-						const u16x2 qa =
-							__builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17))
-							<< (u16x2)(3);
+						u16x2 qa;
+						if (AIRS_KEEP_Q) {
+							qa = pk(mq[0][j]);
+						} else {
+							const u16x2 v = __builtin_elementwise_add_sat(pk(mp[0][j]), (u16x2)(1));
+							qa = __builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17))
+							     << (u16x2)(3);
+						}
 #pragma unroll
 						for (uint32_t h = 0; h < 2; h++)
 							te[2 * jj + h] = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
@@ -1130,6 +1132,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 #pragma unroll
 			for (uint32_t i = 0; i < AIRS_PT / 2; i++) {
 				mp[k][i] = mp[k + 1][i];
+				if (AIRS_KEEP_Q)
+					mq[AIRS_KEEP_Q ? k : 0][i] = mq[AIRS_KEEP_Q ? k + 1 : 0][i];
 				if (MODEL)
 					nmp[k][i] = nmp[k + 1][i];
 			}
