@@ -198,6 +198,15 @@ static int model_needed(const struct cmp_params *p)
 	return p->secondary_preprocessing == CMP_PREPROCESS_MODEL && p->secondary_iterations != 0;
 }
 
+/* some pass of the context keeps state in its work buffer: the model, or the
+ * IWT coefficients (preprocess.c:321-353 computes them into work_buf), so
+ * frames of one context cannot share a launch */
+static int work_buf_state(const struct cmp_params *p)
+{
+	return model_needed(p) || p->primary_preprocessing == CMP_PREPROCESS_IWT ||
+	       (p->secondary_iterations && p->secondary_preprocessing == CMP_PREPROCESS_IWT);
+}
+
 /* cmp_reset; with `draws` set the identifier draw is only counted (the batch
  * API draws the identifiers afterwards, in the reference's call order) */
 static uint32_t ctx_reset(struct cmp_context *ctx, uint32_t *draws)
@@ -362,10 +371,6 @@ static uint32_t engine_prologue(struct cmp_context *ctx, void *dst, uint32_t cap
 	} else if (p->pre != CMP_PREPROCESS_NONE && p->pre != CMP_PREPROCESS_DIFF) {
 		return ERRV(PARAMS_INVALID);
 	}
-	if (p->pre == CMP_PREPROCESS_IWT) {
-		fprintf(stderr, "airscmp: IWT preprocessing is not implemented on the GPU yet\n");
-		return ERRV(GENERIC);
-	}
 	p->model_mode = model_needed(&ctx->params) ?
 				(ctx->sequence_number == 0 ? AIRS_MODEL_STORE : AIRS_MODEL_UPDATE) :
 				AIRS_MODEL_NONE;
@@ -416,9 +421,13 @@ static uint32_t host_engine(struct cmp_context *ctx, void *dst, uint32_t cap, co
 		return ERRV(GENERIC);
 	if (is_err(airs_dev_h2d(dev, d_src, io->src, (size_t)io->n * io->bytes)))
 		return ERRV(GENERIC);
-	if (p.model_mode != AIRS_MODEL_NONE) {
+	if (p.model_mode != AIRS_MODEL_NONE || p.pre == CMP_PREPROCESS_IWT) {
+		/* the work buffer on the device: the model, or the IWT coefficients
+		 * (computed there by the launch, so not uploaded) */
 		d_model = airs_dev_scratch(dev, SLOT_MODEL, (size_t)packed + 16u);
-		if (!d_model || is_err(airs_dev_h2d(dev, d_model, ctx->work_buf, packed)))
+		if (!d_model)
+			return ERRV(GENERIC);
+		if (p.pre != CMP_PREPROCESS_IWT && is_err(airs_dev_h2d(dev, d_model, ctx->work_buf, packed)))
 			return ERRV(GENERIC);
 	}
 	if (ctx->params.checksum_enabled) {
@@ -456,7 +465,9 @@ static uint32_t host_engine(struct cmp_context *ctx, void *dst, uint32_t cap, co
 		return e;
 	if (is_err(airs_dev_d2h(dev, st, d_status, sizeof(st))))
 		return ERRV(GENERIC);
-	if (p.model_mode != AIRS_MODEL_NONE && is_err(airs_dev_d2h(dev, ctx->work_buf, d_model, packed)))
+	/* work_buf afterwards holds what the reference leaves there: the model,
+	 * or the IWT coefficients (overwritten by the model where it is stored) */
+	if (d_model && is_err(airs_dev_d2h(dev, ctx->work_buf, d_model, packed)))
 		return ERRV(GENERIC);
 	if (is_err(airs_dev_sync(dev)))
 		return ERRV(GENERIC);
@@ -675,7 +686,7 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 			return ERRV(GENERIC);
 		L.ids = d_ids;
 	}
-	if (P->model_mode != AIRS_MODEL_NONE) {
+	if (P->model_mode != AIRS_MODEL_NONE || P->pre == CMP_PREPROCESS_IWT) {
 		for (j = 0; j < cnt; j++)
 			ptr_scratch[j] = (uint64_t)(uintptr_t)ctx[FRAME_AT(j) / fpc].work_buf;
 		/* model of frame f = base + (f / fpc) * stride when the work buffers are strided */
@@ -720,7 +731,7 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 		if (is_err(e))
 			return e;
 	}
-	if ((b->flags & CMP_GPU_AUTO_RICE) && P->enc == CMP_ENCODER_GOLOMB_ZERO) {
+	if ((b->flags & CMP_GPU_AUTO_RICE) && P->enc == CMP_ENCODER_GOLOMB_ZERO && P->pre != CMP_PREPROCESS_IWT) {
 		d_g = airs_dev_scratch(dev, SLOT_G, (size_t)nframes_total * 4u);
 		if (!d_g)
 			return ERRV(GENERIC);
@@ -979,7 +990,7 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		if (ctx[c].params.uncompressed_fallback_enabled &&
 		    b->dst_capacity >= raw_frame_size(&ctx[c], n))
 			exact = 1;
-		if (model_needed(&ctx[c].params)) {
+		if (work_buf_state(&ctx[c].params)) {
 			any_model = 1;
 			if ((uintptr_t)ctx[c].work_buf & 1u)
 				return ERRV(WORK_BUF_UNALIGNED);

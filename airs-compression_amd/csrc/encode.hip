@@ -65,7 +65,7 @@
 
 namespace airs {
 
-enum { PRE_NONE = 0, PRE_DIFF = 1, PRE_MODEL = 3 };
+enum { PRE_NONE = 0, PRE_DIFF = 1, PRE_IWT = 2, PRE_MODEL = 3 };
 enum { ENC_RAW = 0, ENC_ZERO = 1, ENC_MULTI = 2 };
 
 struct KArgs {
@@ -514,14 +514,19 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	dbg_stamp(a, gseg, 0);
 
 	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
+	// PRE_IWT: the residuals are the frame's IWT coefficients, computed into
+	// the work buffer by iwt_frame_kernel (reference preprocess.c:321-353);
+	// the samples themselves are only needed to store the model (MODEL == 1)
+	constexpr bool LOADM = MODEL == 2 || PRE == PRE_IWT;
+	constexpr bool NEEDX = !(PRE == PRE_IWT && MODEL == 0);
 	uint8_t *fmodel = nullptr;
-	if (MODEL)
+	if (MODEL || PRE == PRE_IWT)
 		fmodel = a.model_ptrs ? reinterpret_cast<uint8_t *>(a.model_ptrs[lf])
 				      : a.model + (uint64_t)(frame / a.model_div) * a.model_stride;
 	// FULL launches (host-checked): every segment is whole and every frame and
 	// model base is 16-byte aligned, so no per-lane bounds or alignment tests
 	const bool src_al = FULL || ((uintptr_t)fsrc & 15u) == 0;
-	const bool mod_al = MODEL ? (FULL || ((uintptr_t)fmodel & 15u) == 0) : true;
+	const bool mod_al = (MODEL || PRE == PRE_IWT) ? (FULL || ((uintptr_t)fmodel & 15u) == 0) : true;
 
 	// ---- phase 0: issue every load of the segment -----------------------
 	uint32_t firstc[CH];
@@ -532,7 +537,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	for (uint32_t c = 0; c < CH; c++) {
 		firstc[c] = sif * SEGN + c * AIRS_SEG + tid * AIRS_PT;
 		const bool full = FULL || firstc[c] + AIRS_PT <= n;
-		if (full && src_al) {
+		if (NEEDX && full && src_al) {
 			const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)firstc[c] * W);
 			if (DBG(512u)) { // ablation: no HBM reads (synthetic in-register data)
 #pragma unroll
@@ -545,7 +550,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 					raw[c][q] = p[q];
 			}
 		}
-		if (MODEL == 2 && full && mod_al) {
+		if (LOADM && full && mod_al) {
 			const uint4 *p = reinterpret_cast<const uint4 *>(fmodel + (size_t)firstc[c] * 2u);
 			mraw[c][0] = p[0];
 			mraw[c][1] = p[1];
@@ -588,7 +593,11 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		const uint32_t first = firstc[c];
 		nv[c] = FULL ? (uint32_t)AIRS_PT : first >= n ? 0u : min(n - first, (uint32_t)AIRS_PT);
 		uint32_t w[AIRS_PT / 2]; // sample pairs (x[2j] | x[2j+1] << 16)
-		if (nv[c] == AIRS_PT && src_al) {
+		if (!NEEDX) {
+#pragma unroll
+			for (uint32_t j = 0; j < AIRS_PT / 2; j++)
+				w[j] = 0u;
+		} else if (nv[c] == AIRS_PT && src_al) {
 			if (W == 2) {
 				const uint32_t w8[8] = {raw[c][0].x, raw[c][0].y, raw[c][0].z, raw[c][0].w,
 							raw[c][1].x, raw[c][1].y, raw[c][1].z, raw[c][1].w};
@@ -616,8 +625,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				w[j] = x2[0] | x2[1] << 16;
 			}
 		}
-		uint32_t pm[AIRS_PT / 2]; // model pairs (MODEL == 2)
-		if (MODEL == 2) {
+		uint32_t pm[AIRS_PT / 2]; // model pairs (MODEL == 2) or IWT coefficient pairs
+		if (LOADM) {
 			if (nv[c] == AIRS_PT && mod_al) {
 				const uint32_t w8[8] = {mraw[c][0].x, mraw[c][0].y, mraw[c][0].z, mraw[c][0].w,
 							mraw[c][1].x, mraw[c][1].y, mraw[c][1].z, mraw[c][1].w};
@@ -650,6 +659,8 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
 			else if (PRE == PRE_MODEL)
 				u = unpk(pk(w[j]) - pk(pm[j]));
+			else if (PRE == PRE_IWT)
+				u = pm[j];
 			else
 				u = w[j];
 			mp[c][j] = (DBG(8192u)) ? w[j] : (ENC == ENC_RAW ? u : zigzag_pk(u));
@@ -1179,6 +1190,130 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 }
 
 // ---------------------------------------------------------------------
+// Multi-level integer wavelet transform (reference preprocess.c:140-221,
+// iwt_init :321-353): levels with stride s = 1, 2, 4, ... < n, each a lifting
+// step in place: first every odd coefficient (index s mod 2s) from its even
+// neighbours, then every even one from the new odd neighbours.  All values
+// are int16 with the reference's int32 intermediates and int16 wrap.  The
+// coefficients go to the frame's work buffer, where the encoder reads them as
+// its residuals (iwt_process :366-371).
+// ---------------------------------------------------------------------
+__device__ __forceinline__ int16_t iwt_odd(int32_t c, int32_t l, int32_t r)
+{
+	return (int16_t)(c - (int16_t)((l + r) >> 1)); // iwt_odd_coefficient :67-70
+}
+
+__device__ __forceinline__ int16_t iwt_even(int32_t c, int32_t l, int32_t r)
+{
+	return (int16_t)(c + (int16_t)((l + r) >> 2)); // iwt_even_coefficient :96-100
+}
+
+__device__ __forceinline__ int16_t iwt_edge(int32_t c, int32_t nb)
+{
+	return (int16_t)(c + (int16_t)(nb >> 1)); // iwt_edge_even_coefficient :112-115
+}
+
+// odd coefficients of level s for t = t0, t0 + dt, ... (index i = s + 2 s t)
+template <typename P>
+__device__ __forceinline__ void iwt_odds(P y, uint32_t n, uint32_t s, uint32_t t0, uint32_t dt)
+{
+	for (uint32_t t = t0;; t += dt) {
+		const uint64_t i = (uint64_t)s + 2ull * s * t;
+		if (i >= n)
+			break;
+		// the last odd coefficient has no right neighbour (:81-84)
+		y[i] = i + s < n ? iwt_odd(y[i], y[i - s], y[i + s]) : (int16_t)(y[i] - y[i - s]);
+	}
+}
+
+// even coefficients of level s (index i = 2 s t); needs the level's odds
+template <typename P>
+__device__ __forceinline__ void iwt_evens(P y, uint32_t n, uint32_t s, uint32_t t0, uint32_t dt)
+{
+	for (uint32_t t = t0;; t += dt) {
+		const uint64_t i = 2ull * s * t;
+		if (i >= n)
+			break;
+		if (i == 0)
+			y[0] = iwt_edge(y[0], y[s]);
+		else if (i + s < n)
+			y[i] = iwt_even(y[i], y[i - s], y[i + s]);
+		else
+			y[i] = iwt_edge(y[i], y[i - s]);
+	}
+}
+
+struct IwtArgs {
+	const uint8_t *src;
+	uint64_t src_stride;
+	uint8_t *coef; // work buffers: frame f's at coef + (f / coef_div) * coef_stride, or coef_ptrs[j]
+	uint64_t coef_stride;
+	const uint64_t *coef_ptrs;
+	const uint32_t *frame_list;
+	uint32_t frame_add, frame_mul, coef_div;
+	uint32_t n;
+};
+
+__device__ __forceinline__ int16_t *iwt_frame_coef(const IwtArgs &a, uint32_t j, uint32_t *frame)
+{
+	*frame = a.frame_list ? a.frame_list[j] : a.frame_add + j * a.frame_mul;
+	return reinterpret_cast<int16_t *>(a.coef_ptrs ? reinterpret_cast<uint8_t *>(a.coef_ptrs[j])
+						       : a.coef + (uint64_t)(*frame / a.coef_div) * a.coef_stride);
+}
+
+template <int W>
+__device__ __forceinline__ int16_t iwt_sample(const uint8_t *fsrc, uint32_t i)
+{
+	return W == 2 ? reinterpret_cast<const int16_t *>(fsrc)[i]
+		      : (int16_t)(reinterpret_cast<const uint32_t *>(fsrc)[i] & 0xFFFFu); // sample_read_i16
+}
+
+// whole frame in LDS (n <= AIRS_IWT_LDS_MAX): one 1024-thread workgroup per frame
+#define AIRS_IWT_LDS_MAX 65536u
+template <int W>
+__global__ __launch_bounds__(1024) void iwt_frame_kernel(IwtArgs a)
+{
+	extern __shared__ int16_t L_iwt[];
+	uint32_t frame;
+	int16_t *coef = iwt_frame_coef(a, blockIdx.x, &frame);
+	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
+	const uint32_t n = a.n, tid = threadIdx.x;
+	for (uint32_t i = tid; i < n; i += 1024u)
+		L_iwt[i] = iwt_sample<W>(fsrc, i);
+	__syncthreads();
+	for (uint32_t s = 1; s < n; s <<= 1) {
+		iwt_odds(L_iwt, n, s, tid, 1024u);
+		__syncthreads();
+		iwt_evens(L_iwt, n, s, tid, 1024u);
+		__syncthreads();
+	}
+	for (uint32_t i = tid; i < n; i += 1024u)
+		coef[i] = L_iwt[i];
+}
+
+// larger frames: samples -> work buffer, then two launches per level
+template <int W>
+__global__ __launch_bounds__(256) void iwt_copy_kernel(IwtArgs a)
+{
+	uint32_t frame;
+	int16_t *coef = iwt_frame_coef(a, blockIdx.y, &frame);
+	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
+	for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += gridDim.x * 256u)
+		coef[i] = iwt_sample<W>(fsrc, i);
+}
+
+__global__ __launch_bounds__(256) void iwt_level_kernel(IwtArgs a, uint32_t s, uint32_t evens)
+{
+	uint32_t frame;
+	int16_t *coef = iwt_frame_coef(a, blockIdx.y, &frame);
+	const uint32_t t0 = blockIdx.x * 256u + threadIdx.x, dt = gridDim.x * 256u;
+	if (evens)
+		iwt_evens(coef, a.n, s, t0, dt);
+	else
+		iwt_odds(coef, a.n, s, t0, dt);
+}
+
+// ---------------------------------------------------------------------
 // XXH32 per frame over big-endian 16-bit samples (reference header.c:137-163).
 // The four accumulators of a frame run in four lanes; each stripe is 8
 // samples = 16 bytes, lane q consumes bytes 4q..4q+3 of every stripe.
@@ -1548,6 +1683,11 @@ static void dispatch_pre(const KArgs &k, uint32_t pre, uint32_t enc, bool rice, 
 {
 	if (pre == PRE_MODEL) {
 		dispatch_enc<W, PRE_MODEL, AIRS_MODEL_UPDATE>(k, enc, rice, full, grid, s);
+	} else if (pre == PRE_IWT) {
+		if (model_mode == AIRS_MODEL_STORE)
+			dispatch_enc<W, PRE_IWT, AIRS_MODEL_STORE>(k, enc, rice, full, grid, s);
+		else
+			dispatch_enc<W, PRE_IWT, AIRS_MODEL_NONE>(k, enc, rice, full, grid, s);
 	} else if (pre == PRE_DIFF) {
 		if (model_mode == AIRS_MODEL_STORE)
 			dispatch_enc<W, PRE_DIFF, AIRS_MODEL_STORE>(k, enc, rice, full, grid, s);
@@ -1561,11 +1701,66 @@ static void dispatch_pre(const KArgs &k, uint32_t pre, uint32_t enc, bool rice, 
 	}
 }
 
+// IWT coefficients of every launch frame into its work buffer (the model
+// addressing of the launch), ahead of the encode kernel
+static uint32_t run_iwt(struct airs_dev_engine *e, const struct airs_launch *L)
+{
+	IwtArgs a;
+	memset(&a, 0, sizeof(a));
+	a.src = (const uint8_t *)L->src;
+	a.src_stride = L->src_stride;
+	a.coef = (uint8_t *)L->model;
+	a.coef_stride = L->model_stride;
+	a.coef_ptrs = L->model_ptrs;
+	a.coef_div = L->model_div ? L->model_div : 1u;
+	a.frame_list = L->frame_list;
+	a.frame_add = L->frame_add;
+	a.frame_mul = L->frame_list ? 0u : L->frame_mul;
+	a.n = L->n;
+	const bool w2 = L->sample_bytes == 2;
+	if (L->n <= AIRS_IWT_LDS_MAX) {
+		static bool attr = false;
+		if (!attr) {
+			const int mx = (int)(AIRS_IWT_LDS_MAX * 2u);
+			HIPCHECK(hipFuncSetAttribute((const void *)iwt_frame_kernel<2>,
+						     hipFuncAttributeMaxDynamicSharedMemorySize, mx));
+			HIPCHECK(hipFuncSetAttribute((const void *)iwt_frame_kernel<4>,
+						     hipFuncAttributeMaxDynamicSharedMemorySize, mx));
+			attr = true;
+		}
+		const size_t lds = (size_t)L->n * 2u;
+		if (w2)
+			hipLaunchKernelGGL(iwt_frame_kernel<2>, dim3(L->num_frames), dim3(1024), lds, e->stream, a);
+		else
+			hipLaunchKernelGGL(iwt_frame_kernel<4>, dim3(L->num_frames), dim3(1024), lds, e->stream, a);
+		HIPCHECK(hipGetLastError());
+		return 0;
+	}
+	if (L->num_frames > 65535u)
+		return ERRV(E_PARAMS_INVALID);
+	const uint32_t cb = min((L->n + 255u) / 256u, 1024u);
+	if (w2)
+		hipLaunchKernelGGL(iwt_copy_kernel<2>, dim3(cb, L->num_frames), dim3(256), 0, e->stream, a);
+	else
+		hipLaunchKernelGGL(iwt_copy_kernel<4>, dim3(cb, L->num_frames), dim3(256), 0, e->stream, a);
+	for (uint32_t st = 1; st < L->n; st <<= 1) {
+		const uint32_t items = (uint32_t)(((uint64_t)L->n + 2ull * st - 1ull) / (2ull * st));
+		const uint32_t gb = min((items + 255u) / 256u, 1024u);
+		hipLaunchKernelGGL(iwt_level_kernel, dim3(gb, L->num_frames), dim3(256), 0, e->stream, a, st, 0u);
+		hipLaunchKernelGGL(iwt_level_kernel, dim3(gb, L->num_frames), dim3(256), 0, e->stream, a, st, 1u);
+	}
+	HIPCHECK(hipGetLastError());
+	return 0;
+}
+
 extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L)
 {
 	if (!e || !L || L->n == 0 || L->num_frames == 0)
 		return ERRV(E_GENERIC);
-	if (L->preprocessing != PRE_NONE && L->preprocessing != PRE_DIFF && L->preprocessing != PRE_MODEL)
+	if (L->preprocessing > PRE_MODEL)
+		return ERRV(E_PARAMS_INVALID);
+	if (L->preprocessing == PRE_IWT && (L->frame_g || L->model_mode == AIRS_MODEL_UPDATE ||
+					    (!L->model && !L->model_ptrs)))
 		return ERRV(E_PARAMS_INVALID);
 	if (L->encoder_type > ENC_MULTI || (L->sample_bytes != 2 && L->sample_bytes != 4))
 		return ERRV(E_PARAMS_INVALID);
@@ -1667,9 +1862,14 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 		    (L->encoder_param && (L->encoder_param & (L->encoder_param - 1u)) == 0u);
 	if (L->preprocessing == PRE_MODEL && L->model_mode != AIRS_MODEL_UPDATE)
 		return ERRV(E_PARAMS_INVALID);
+	if (L->preprocessing == PRE_IWT) {
+		r = run_iwt(e, L);
+		if (r)
+			return r;
+	}
 	// whole segments and 16-byte aligned frames (and models): the FULL kernel
 	bool full = L->n % segn == 0u && ((uintptr_t)L->src & 15u) == 0u && (L->src_stride & 15u) == 0u;
-	if (L->model_mode != AIRS_MODEL_NONE)
+	if (L->model_mode != AIRS_MODEL_NONE || L->preprocessing == PRE_IWT)
 		full = full && (L->model_ptrs ? L->model_ptrs_al16 != 0u
 					      : ((uintptr_t)L->model & 15u) == 0u && (L->model_stride & 15u) == 0u);
 	if (L->sample_bytes == 2)

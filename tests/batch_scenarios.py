@@ -26,7 +26,7 @@ def _ts_counter(start):
 def make_case(api, trial):
     """Seeded batch case: params, kind, n, nctx, fpc, cap, per-frame sources."""
     rng = random.Random(trial)
-    params = scenarios.make_params(api.CmpParams, rng, allow_iwt=False)
+    params = scenarios.make_params(api.CmpParams, rng, allow_iwt=True)
     params.uncompressed_fallback_enabled = rng.choice([0, 1, 1])
     kind = rng.choice(scenarios.KINDS)
     n = rng.choice([1, 7, 64, 333, 4095, 4097, 9000])

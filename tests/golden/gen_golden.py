@@ -117,6 +117,19 @@ for kind in ("u16", "i16", "i16_in_i32"):
                              dict(src=[0, 0, 0, 0], payload="AA",
                                   hdr=dict(preprocessing=1, encoder_type=1, encoder_param=1,
                                            encoder_outlier=16))]))
+# IWT transform KATs (test/test_preprocessing.c:74-144): UNCOMPRESSED + IWT,
+# the payload is the multi-level coefficients as big-endian int16
+IWT_CASES = [([42], [42]), ([-23809, 23901], [-32722, -17826]), ([-1, 2, -3, 4, -5], [0, 4, 0, 8, -2]),
+             ([0, 0, 2, 0, 0, 0, 0], [-1, -1, 2, -1, -1, 0, 1]),
+             ([-3, 2, -1, 3, -2, 5, 0, 7], [0, 4, 2, 5, 1, 6, 3, 7])]
+for vals, exp in IWT_CASES:
+    for kind in ("u16", "i16", "i16_in_i32"):
+        KATS.append(dict(name="iwt_%d_%s" % (len(vals), kind), source="test/test_preprocessing.c:74-144",
+                         kind=kind, cap=None, work=True,
+                         params=dict(primary_encoder_type=RAW, primary_preprocessing=2),
+                         frames=[dict(src=[v & (0xFFFFFFFF if kind == "i16_in_i32" else 0xFFFF) for v in vals],
+                                      payload="".join("%04X" % (v & 0xFFFF) for v in exp),
+                                      hdr=dict(preprocessing=2, encoder_type=0))]))
 # examples/simple_compression.c:58-322 (dummy timestamp: fine counter from 1)
 EXAMPLE = dict(name="simple_compression_example", source="examples/simple_compression.c:101-296",
                kind="u16", cap="bound", work=True, timestamp="example",

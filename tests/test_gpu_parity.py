@@ -43,25 +43,23 @@ def test_kat_gpu(gpu, kat):
 
 
 def test_random_sequences_gpu_vs_golden(gpu):
-    """Reference digests for every scenario without IWT (IWT is not on the GPU yet)."""
+    """Reference digests for every golden scenario (IWT included): frames,
+    context fields and the work buffer after every call."""
     bad, ran = [], 0
     for case in SEQS:
-        p = case["params"]
-        if p["primary_preprocessing"] == 2 or (p["secondary_iterations"] and p["secondary_preprocessing"] == 2):
-            continue
         params, kind, n = scenarios.random_case(api.CmpParams, case["trial"], allow_iwt=True)
         res = scenarios.run_sequence(gpu, params, kind, n, seed=case["trial"])
         ran += 1
         if hashlib.sha256(repr(res).encode()).hexdigest() != case["digest"]:
             bad.append(case["trial"])
-    assert ran > 200
+    assert ran == len(SEQS) >= 400
     assert not bad, f"GPU differs from the reference on trials {bad[:10]}"
 
 
 def test_random_sequences_gpu_vs_oracle(gpu, orc):
     bad = []
     for trial in range(20000, 20400):
-        params, kind, n = scenarios.random_case(api.CmpParams, trial, allow_iwt=False)
+        params, kind, n = scenarios.random_case(api.CmpParams, trial, allow_iwt=True)
         a = scenarios.run_sequence(gpu, params, kind, n, seed=trial)
         b = scenarios.run_sequence(orc, params, kind, n, seed=trial)
         if a != b:
@@ -90,6 +88,50 @@ def test_segment_boundaries_vs_oracle(gpu, orc):
                 outs.append((r, bytes(dst[:r]) if not api.is_error(r) else None))
                 lib.set_timestamp_func(None)
             assert outs[0] == outs[1], (n, pre, enc, g)
+
+
+@pytest.mark.parametrize("kind", scenarios.KINDS)
+def test_iwt_sizes_vs_oracle(gpu, orc, kind):
+    """IWT preprocessing (reference preprocess.c:140-221, 321-371) at level and
+    kernel boundaries: the whole-frame LDS kernel up to 65536 samples, the
+    per-level global kernels above; primary IWT with and without a MODEL
+    secondary (the model overwrites the coefficients in the work buffer as
+    the samples are encoded), and IWT as the secondary pass."""
+    sb = 4 if kind == "i16_in_i32" else 2
+    for n in (1, 2, 3, 4, 5, 6, 7, 9, 16, 17, 33, 1000, 4095, 4097, 65535, 65536, 65537, 131075, 300001):
+        for prm in (dict(primary_preprocessing=2, primary_encoder_type=1, primary_encoder_param=16),
+                    dict(primary_preprocessing=2, primary_encoder_type=2, primary_encoder_param=10,
+                         primary_encoder_outlier=200, secondary_iterations=2, secondary_preprocessing=3,
+                         secondary_encoder_type=2, secondary_encoder_param=8, secondary_encoder_outlier=107,
+                         model_rate=11, checksum_enabled=1),
+                    dict(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=32,
+                         secondary_iterations=1, secondary_preprocessing=2, secondary_encoder_type=0)):
+            if n > 70000 and prm.get("secondary_iterations") == 2:
+                continue
+            outs = []
+            for lib in (gpu, orc):
+                p = api.CmpParams(**prm)
+                ctx = api.CmpContext()
+                wbs = lib.cal_work_buf_size(p, n * sb)
+                wb = api.aligned_empty(max(wbs, 2), fill=0x5A)
+                lib.set_timestamp_func(lambda: (1, 2))
+                assert not api.is_error(lib.initialise(ctx, p, wb, wbs))
+                res = []
+                r2 = np.random.default_rng(n)
+                for step in range(3):
+                    x = np.cumsum(r2.integers(-900, 900, n)) & 0xFFFF
+                    x[r2.integers(0, n, max(1, n // 100))] = r2.integers(0, 65536, max(1, n // 100))
+                    if kind == "i16_in_i32":
+                        x = (x | (r2.integers(0, 65536, n) << 16)).astype(np.uint32).view(np.int32)
+                    else:
+                        x = x.astype(np.uint16) if kind == "u16" else x.astype(np.uint16).view(np.int16)
+                    cap = 3 * 2 * n + 64 if step != 1 else 16 + n  # step 1: too small (fallback off)
+                    dst = api.aligned_empty(cap + 64, fill=0xAB)
+                    r = lib.compress(kind, ctx, dst, cap, x)
+                    res.append((r, bytes(dst[:r]) if not api.is_error(r) else None, bytes(wb)))
+                lib.set_timestamp_func(None)
+                outs.append(res)
+            assert outs[0] == outs[1], (kind, n, prm)
 
 
 def test_gpu_synth_matches_oracle(eng, orc_ext):
