@@ -44,6 +44,13 @@
 #endif
 #define AIRS_PT 16
 #define AIRS_SEG (AIRS_WG * AIRS_PT)
+// encode kernel: EWG threads per workgroup, EPT samples per lane per chunk
+// (EWG * EPT = AIRS_SEG samples per chunk)
+#ifndef AIRS_EWG
+#define AIRS_EWG 256
+#endif
+#define EWG AIRS_EWG
+#define EPT (AIRS_SEG / AIRS_EWG)
 // bounded spins: ~2^22 polls with s_sleep is far beyond any legitimate wait
 #define AIRS_SPIN_LIMIT (1u << 22)
 // engine->ticket[AIRS_FAULT_WORD] counts look-back give-ups (must stay 0)
@@ -459,8 +466,13 @@ __host__ __device__ constexpr uint32_t seg_images(int W, int MODEL)
 	return (seg_chunks(W, MODEL) >= 4u && !MODEL) ? AIRS_NIMG : 2u;
 }
 
+#ifdef AIRS_EWPE // minimum waves per SIMD the register allocation must allow
+#define AIRS_EWPE_ATTR __attribute__((amdgpu_waves_per_eu(AIRS_EWPE, 8)))
+#else
+#define AIRS_EWPE_ATTR
+#endif
 template <int W, int PRE, int ENC, bool RICE, int MODEL, bool FULL>
-__global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
+__global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 {
 	constexpr uint32_t CH = seg_chunks(W, MODEL);
 	constexpr uint32_t SEGN = CH * AIRS_SEG;
@@ -472,14 +484,15 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// 0 with a model, whose chunk-0 update needs the bit offset first.
 	constexpr uint32_t NIMG = seg_images(W, MODEL);
 	constexpr uint32_t LBC = (MODEL || CH < 2) ? 0u : NIMG - 1u;
-	constexpr uint32_t RW = W == 2 ? 2u : 4u; // uint4 per lane per chunk
+	constexpr uint32_t RW = EPT * W / 16u; // uint4 per lane per chunk
+	constexpr uint32_t MRW = EPT / 8u;      // uint4 of 16-bit model values per lane per chunk
 	constexpr bool EXT_HDR = !(PRE == PRE_NONE && ENC == ENC_RAW);
 	constexpr uint32_t HDR_BITS = EXT_HDR ? 176u : 128u;
 	// NIMG chunk images in dynamic LDS, a.img_words each (sized per launch from
 	// the longest codeword the pass can emit), each after a 4-word guard
 	extern __shared__ __attribute__((aligned(16))) uint32_t L_dyn[];
 	const uint32_t IMGW = a.img_words + 4u; // words per image incl. guard (multiple of 4)
-	__shared__ uint32_t s_wsum[CH][AIRS_WG / 64];
+	__shared__ uint32_t s_wsum[CH][EWG / 64];
 	__shared__ uint32_t s_misc[8];
 	// Rice/ZERO code table (fast path): entry q' = min(q, 17) holds
 	// {T'[q'], len[q']} with codeword = m + T'[q'] (see rice_table)
@@ -531,12 +544,12 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// ---- phase 0: issue every load of the segment -----------------------
 	uint32_t firstc[CH];
 	uint4 raw[CH][RW];
-	uint4 mraw[CH][2];
+	uint4 mraw[CH][MRW];
 	uint32_t prevld[CH];
 #pragma unroll
 	for (uint32_t c = 0; c < CH; c++) {
-		firstc[c] = sif * SEGN + c * AIRS_SEG + tid * AIRS_PT;
-		const bool full = FULL || firstc[c] + AIRS_PT <= n;
+		firstc[c] = sif * SEGN + c * AIRS_SEG + tid * EPT;
+		const bool full = FULL || firstc[c] + EPT <= n;
 		if (NEEDX && full && src_al) {
 			const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)firstc[c] * W);
 			if (DBG(512u)) { // ablation: no HBM reads (synthetic in-register data)
@@ -552,8 +565,9 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		}
 		if (LOADM && full && mod_al) {
 			const uint4 *p = reinterpret_cast<const uint4 *>(fmodel + (size_t)firstc[c] * 2u);
-			mraw[c][0] = p[0];
-			mraw[c][1] = p[1];
+#pragma unroll
+			for (uint32_t q = 0; q < MRW; q++)
+				mraw[c][q] = p[q];
 		}
 		prevld[c] = 0u;
 		if (PRE == PRE_DIFF && lane == 0u && firstc[c] != 0u && firstc[c] <= n && !(DBG(512u)))
@@ -564,7 +578,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	// zero both LDS chunk images while the loads are in flight
 	{
 		uint4 *L4 = reinterpret_cast<uint4 *>(L_dyn);
-		for (uint32_t i = tid; i < ((DBG(4096u)) ? 0u : NIMG * IMGW / 4u); i += AIRS_WG)
+		for (uint32_t i = tid; i < ((DBG(4096u)) ? 0u : NIMG * IMGW / 4u); i += EWG)
 			L4[i] = make_uint4(0u, 0u, 0u, 0u);
 	}
 
@@ -579,41 +593,43 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	const bool fastk = ENC == ENC_ZERO && RICE && cd.k <= 11u;
 	if (fastk && tid < 18u)
 		s_rice[tid] = rice_table_entry(tid, cd.k);
-	uint32_t mp[CH][AIRS_PT / 2]; // mapped values, two 16-bit per register
+	uint32_t mp[CH][EPT / 2]; // mapped values, two 16-bit per register
 	// Rice/ZERO fast path (AIRS_KEEP_Q): the code-table byte offsets
 	// 8 min(q, 17) of every pair, computed once in phase 1 next to the lengths
 #ifndef AIRS_KEEP_Q
 #define AIRS_KEEP_Q 1
 #endif
-	uint32_t mq[AIRS_KEEP_Q ? CH : 1][AIRS_PT / 2];
-	uint32_t nmp[MODEL ? CH : 1][AIRS_PT / 2]; // new model values (MODEL)
+	uint32_t mq[AIRS_KEEP_Q ? CH : 1][EPT / 2];
+	uint32_t nmp[MODEL ? CH : 1][EPT / 2]; // new model values (MODEL)
 	uint32_t T[CH], nv[CH];
 #pragma unroll
 	for (uint32_t c = 0; c < CH; c++) {
 		const uint32_t first = firstc[c];
-		nv[c] = FULL ? (uint32_t)AIRS_PT : first >= n ? 0u : min(n - first, (uint32_t)AIRS_PT);
-		uint32_t w[AIRS_PT / 2]; // sample pairs (x[2j] | x[2j+1] << 16)
+		nv[c] = FULL ? (uint32_t)EPT : first >= n ? 0u : min(n - first, (uint32_t)EPT);
+		uint32_t w[EPT / 2]; // sample pairs (x[2j] | x[2j+1] << 16)
 		if (!NEEDX) {
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT / 2; j++)
+			for (uint32_t j = 0; j < EPT / 2; j++)
 				w[j] = 0u;
-		} else if (nv[c] == AIRS_PT && src_al) {
+		} else if (nv[c] == EPT && src_al) {
 			if (W == 2) {
-				const uint32_t w8[8] = {raw[c][0].x, raw[c][0].y, raw[c][0].z, raw[c][0].w,
-							raw[c][1].x, raw[c][1].y, raw[c][1].z, raw[c][1].w};
 #pragma unroll
-				for (int j = 0; j < 8; j++)
-					w[j] = w8[j];
+				for (uint32_t q = 0; q < RW; q++) {
+					w[4 * q] = raw[c][q].x;
+					w[4 * q + 1] = raw[c][q].y;
+					w[4 * q + 2] = raw[c][q].z;
+					w[4 * q + 3] = raw[c][q].w;
+				}
 			} else {
 #pragma unroll
-				for (uint32_t q = 0; q < 4; q++) {
+				for (uint32_t q = 0; q < RW; q++) {
 					w[2 * q] = __builtin_amdgcn_perm(raw[c][q].y, raw[c][q].x, 0x05040100u);
 					w[2 * q + 1] = __builtin_amdgcn_perm(raw[c][q].w, raw[c][q].z, 0x05040100u);
 				}
 			}
 		} else {
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+			for (uint32_t j = 0; j < EPT / 2; j++) {
 				uint32_t x2[2];
 #pragma unroll
 				for (uint32_t h = 0; h < 2; h++) {
@@ -625,17 +641,19 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				w[j] = x2[0] | x2[1] << 16;
 			}
 		}
-		uint32_t pm[AIRS_PT / 2]; // model pairs (MODEL == 2) or IWT coefficient pairs
+		uint32_t pm[EPT / 2]; // model pairs (MODEL == 2) or IWT coefficient pairs
 		if (LOADM) {
-			if (nv[c] == AIRS_PT && mod_al) {
-				const uint32_t w8[8] = {mraw[c][0].x, mraw[c][0].y, mraw[c][0].z, mraw[c][0].w,
-							mraw[c][1].x, mraw[c][1].y, mraw[c][1].z, mraw[c][1].w};
+			if (nv[c] == EPT && mod_al) {
 #pragma unroll
-				for (int j = 0; j < 8; j++)
-					pm[j] = w8[j];
+				for (uint32_t q = 0; q < MRW; q++) {
+					pm[4 * q] = mraw[c][q].x;
+					pm[4 * q + 1] = mraw[c][q].y;
+					pm[4 * q + 2] = mraw[c][q].z;
+					pm[4 * q + 3] = mraw[c][q].w;
+				}
 			} else {
 #pragma unroll
-				for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+				for (uint32_t j = 0; j < EPT / 2; j++) {
 					uint32_t x2[2];
 #pragma unroll
 					for (uint32_t h = 0; h < 2; h++) {
@@ -648,12 +666,12 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		}
 		uint32_t wprev = 0u; // pair whose high half is the sample before this lane's first
 		if (PRE == PRE_DIFF) {
-			wprev = __shfl_up(w[AIRS_PT / 2 - 1], 1, 64);
+			wprev = __shfl_up(w[EPT / 2 - 1], 1, 64);
 			if (lane == 0u)
 				wprev = prevld[c] << 16;
 		}
 #pragma unroll
-		for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+		for (uint32_t j = 0; j < EPT / 2; j++) {
 			uint32_t u;
 			if (PRE == PRE_DIFF)
 				u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
@@ -667,27 +685,27 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		}
 		uint32_t t = 0u;
 		if (DBG(64u)) {
-			t = AIRS_PT * (cd.k + 1u) + (mp[c][0] & 7u);
-		} else if (fastk && nv[c] == AIRS_PT) {
+			t = EPT * (cd.k + 1u) + (mp[c][0] & 7u);
+		} else if (fastk && nv[c] == EPT) {
 			u16x2 acc = (u16x2)(0);
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+			for (uint32_t j = 0; j < EPT / 2; j++) {
 				const u16x2 v = __builtin_elementwise_add_sat(pk(mp[c][j]), (u16x2)(1));
 				const u16x2 q = v >> (u16x2)((unsigned short)cd.k);
 				acc += __builtin_elementwise_min(q, (u16x2)(16));
 				if (AIRS_KEEP_Q)
 					mq[AIRS_KEEP_Q ? c : 0][j] = unpk(__builtin_elementwise_min(q, (u16x2)(17)) << (u16x2)(3));
 			}
-			t = AIRS_PT * (cd.k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
+			t = EPT * (cd.k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
 		} else {
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT; j++)
+			for (uint32_t j = 0; j < EPT; j++)
 				t += j < nv[c] ? len_from_m<ENC, RICE>(half16(mp[c][j >> 1], j & 1u), cd) : 0u;
 		}
 		T[c] = t;
 		if (MODEL) {
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+			for (uint32_t j = 0; j < EPT / 2; j++) {
 				if (MODEL == 1) {
 					nmp[MODEL ? c : 0][j] = w[j];
 				} else {
@@ -708,11 +726,11 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		// phase 1's per-sample intermediates alive to CSE them with phase 2's
 		// recomputation, which costs ~100 extra VGPRs and halves occupancy.
 #pragma unroll
-		for (uint32_t i = 0; i < AIRS_PT / 2; i++)
+		for (uint32_t i = 0; i < EPT / 2; i++)
 			asm volatile("" : "+v"(mp[c][i]));
 		if (AIRS_KEEP_Q) {
 #pragma unroll
-			for (uint32_t i = 0; i < AIRS_PT / 2; i++)
+			for (uint32_t i = 0; i < EPT / 2; i++)
 				asm volatile("" : "+v"(mq[AIRS_KEEP_Q ? c : 0][i]));
 		}
 	}
@@ -747,7 +765,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 	for (uint32_t c = 0; c < CH; c++) {
 		uint32_t woff = 0u, tt = 0u;
 #pragma unroll
-		for (uint32_t w = 0; w < AIRS_WG / 64; w++) {
+		for (uint32_t w = 0; w < EWG / 64; w++) {
 			const uint32_t v = s_wsum[c][w];
 			woff += w < wid ? v : 0u;
 			tt += v;
@@ -771,13 +789,14 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			lb_prefetch<LB_WIN>(a, gv, tv0, gseg, first_seg, lane);
 		}
 	}
-	if (!is_last && wid == AIRS_WG / 64 - 1 && !(DBG(8u))) {
-		// lane 255 holds >= 16 bits of the last chunk; lane 254 supplies the rest
+	if (!is_last && wid == EWG / 64 - 1 && !(DBG(8u))) {
+		// the last lanes' streams (>= EPT bits each) combined: lane 63 gets
+		// the chunk's last 32 bits
 		uint64_t acc = 0u;
-		if (fastk && nv[CH - 1] == AIRS_PT) {
+		if (fastk && nv[CH - 1] == EPT) {
 			const char *tab = reinterpret_cast<const char *>(s_rice);
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT / 2; j++) {
+			for (uint32_t j = 0; j < EPT / 2; j++) {
 				const u16x2 v = __builtin_elementwise_add_sat(pk(mp[CH - 1][j]), (u16x2)(1));
 				const u16x2 qa = __builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17))
 						 << (u16x2)(3);
@@ -789,7 +808,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			}
 		} else {
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT; j++) {
+			for (uint32_t j = 0; j < EPT; j++) {
 				const uint32_t m = (mp[CH - 1][j >> 1] >> (16u * (j & 1u))) & 0xFFFFu;
 				uint32_t c1, l1, c2, l2;
 				code_from_m<ENC, RICE>(m, cd, c1, l1, c2, l2);
@@ -798,13 +817,20 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 					acc = (acc << l2) | c2;
 			}
 		}
-		const uint32_t lo = (uint32_t)acc;
-		const uint32_t lo_prev = __shfl_up(lo, 1, 64);
-		if (lane == 63u) {
-			const uint32_t tl = T[CH - 1];
-			const uint32_t t32 = tl >= 32u ? lo : ((lo_prev << tl) | (lo & ((1u << tl) - 1u)));
-			gran_store(&a.tail[gseg], ((uint64_t)a.epoch << 32) | t32);
+		// (v, t) = the last min(T, 32) stream bits of a lane run; combining an
+		// earlier run a with a later b is associative: two scan steps cover
+		// four lanes, >= 32 bits for EPT >= 8
+		uint32_t v = (uint32_t)acc, tb = min(T[CH - 1], 32u);
+#pragma unroll
+		for (uint32_t d = 1; d <= 2; d <<= 1) {
+			const uint32_t va = __shfl_up(v, d, 64), ta = __shfl_up(tb, d, 64);
+			if (lane >= d && tb < 32u) {
+				v = (va << tb) | v;
+				tb = min(ta + tb, 32u);
+			}
 		}
+		if (lane == 63u)
+			gran_store(&a.tail[gseg], ((uint64_t)a.epoch << 32) | v);
 	}
 
 	uint32_t last_ne = 0u; // last non-empty chunk
@@ -835,7 +861,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		// 16-byte buffer store (the image is 16-byte aligned, j a multiple of 4)
 		const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)Lx);
 		const uint32_t nquad = (DBG(2048u)) ? 0u : (nfull >> 2);
-		for (uint32_t p = tid; p < nquad; p += AIRS_WG) {
+		for (uint32_t p = tid; p < nquad; p += EWG) {
 			const uint32_t j = 4u * p;
 			const u32x4 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + j);
 			const uint32_t hi = j ? Ll[j - 1u] : predx;
@@ -850,7 +876,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		// the last nfull % 4 words: one each for the threads next in turn
 		// (thread 0 when one of them is word 0, the only word that needs
 		// predx, which lives in lane 0 of wave 0)
-		const uint32_t rr = (tid - nquad) & (AIRS_WG - 1u);
+		const uint32_t rr = (tid - nquad) & (EWG - 1u);
 		if (rr < (nfull & 3u) && !(DBG(2048u))) {
 			const uint32_t j = 4u * nquad + rr;
 			const uint32_t hi = j ? Ll[j - 1u] : predx;
@@ -889,7 +915,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			// image c%NIMG was last read by chunk c-NIMG's stores (before the
 			// barrier that ended chunk c-1's packing): clear what it used
 			const uint32_t nw = (max(NIMG == 2 ? tot_m2 : tot_m3, tot[0]) + 31u) >> 5;
-			for (uint32_t i = tid; i <= ((DBG(4096u)) ? 0u : nw); i += AIRS_WG)
+			for (uint32_t i = tid; i <= ((DBG(4096u)) ? 0u : nw); i += EWG)
 				Lc[i] = 0u;
 			__syncthreads();
 		}
@@ -899,12 +925,12 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 		if (LBC >= 1 && c == (AIRS_LBP) && wid == 0 && !is_first && !(DBG(2u))) {
 			lb_prefetch<LB_WIN>(a, gv, tv0, gseg, first_seg, lane);
 		}
-		uint32_t ln[NPIECE][AIRS_PT]; // piece lengths (kept for the MODEL fail_bit check)
+		uint32_t ln[NPIECE][EPT]; // piece lengths (kept for the MODEL fail_bit check)
 		{
 			Packer pk1;
 			pk1.init(Lc, excl[0]);
 			if (DBG(32u)) {
-			} else if (fastk && nv[0] == AIRS_PT) {
+			} else if (fastk && nv[0] == EPT) {
 				// table-driven: byte offsets 8*min(q, 17) of both samples of a
 				// pair come from three packed ops; codeword = m + T'[q']
 				// (all 16 lookups are issued before the first put: the compiler
@@ -912,10 +938,10 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				const char *tab = reinterpret_cast<const char *>(s_rice);
 #pragma unroll
 				for (uint32_t hb = 0; hb < 2; hb++) { // two batches of 8 lookups
-					uint2 te[AIRS_PT / 2];
+					uint2 te[EPT / 2];
 #pragma unroll
-					for (uint32_t jj = 0; jj < AIRS_PT / 4; jj++) {
-						const uint32_t j = hb * (AIRS_PT / 4) + jj;
+					for (uint32_t jj = 0; jj < EPT / 4; jj++) {
+						const uint32_t j = hb * (EPT / 4) + jj;
 						u16x2 qa;
 						if (AIRS_KEEP_Q) {
 							qa = pk(mq[0][j]);
@@ -934,27 +960,27 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 					// has a longer pair, the whole batch takes two puts per pair.
 					uint32_t mxl = 0u;
 #pragma unroll
-					for (uint32_t i = 0; i < AIRS_PT / 2; i += 2)
+					for (uint32_t i = 0; i < EPT / 2; i += 2)
 						mxl = max(mxl, te[i].y + te[i + 1].y);
 					if (__ballot(mxl > 32u) == 0ull) {
 #pragma unroll
-						for (uint32_t i = 0; i < AIRS_PT / 2; i += 2) {
-							const uint32_t j = hb * (AIRS_PT / 2) + i;
+						for (uint32_t i = 0; i < EPT / 2; i += 2) {
+							const uint32_t j = hb * (EPT / 2) + i;
 							const uint32_t cwa = (mp[0][j >> 1] & 0xFFFFu) + te[i].x;
 							const uint32_t cwb = (mp[0][j >> 1] >> 16) + te[i + 1].x;
 							pk1.put((cwa << te[i + 1].y) | cwb, te[i].y + te[i + 1].y);
 						}
 					} else {
 #pragma unroll
-						for (uint32_t i = 0; i < AIRS_PT / 2; i += 2) {
-							const uint32_t j = hb * (AIRS_PT / 2) + i;
+						for (uint32_t i = 0; i < EPT / 2; i += 2) {
+							const uint32_t j = hb * (EPT / 2) + i;
 							pk1.put((mp[0][j >> 1] & 0xFFFFu) + te[i].x, te[i].y);
 							pk1.put((mp[0][j >> 1] >> 16) + te[i + 1].x, te[i + 1].y);
 						}
 					}
 #pragma unroll
-					for (uint32_t i = 0; i < AIRS_PT / 2; i += 2) {
-						const uint32_t j = hb * (AIRS_PT / 2) + i;
+					for (uint32_t i = 0; i < EPT / 2; i += 2) {
+						const uint32_t j = hb * (EPT / 2) + i;
 						ln[0][j] = te[i].y;
 						ln[0][j + 1] = te[i + 1].y;
 						if (NPIECE == 2) {
@@ -965,7 +991,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 				}
 			} else {
 #pragma unroll
-				for (uint32_t j = 0; j < AIRS_PT; j++) {
+				for (uint32_t j = 0; j < EPT; j++) {
 					const uint32_t m = half16(mp[0][j >> 1], j & 1u);
 					uint32_t c1, l1, c2, l2;
 					code_from_m<ENC, RICE>(m, cd, c1, l1, c2, l2);
@@ -1111,7 +1137,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			bool all_ok = true;
 			uint32_t okmask = 0u;
 #pragma unroll
-			for (uint32_t j = 0; j < AIRS_PT; j++) {
+			for (uint32_t j = 0; j < EPT; j++) {
 #pragma unroll
 				for (uint32_t p = 0; p < NPIECE; p++)
 					bpos += ln[p][j];
@@ -1122,11 +1148,12 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 			uint16_t *mpp = reinterpret_cast<uint16_t *>(fmodel) + firstc[0];
 			if (all_ok && mod_al) {
 				const uint32_t *q = nmp[0];
-				reinterpret_cast<uint4 *>(mpp)[0] = make_uint4(q[0], q[1], q[2], q[3]);
-				reinterpret_cast<uint4 *>(mpp)[1] = make_uint4(q[4], q[5], q[6], q[7]);
+#pragma unroll
+				for (uint32_t r = 0; r < MRW; r++)
+					reinterpret_cast<uint4 *>(mpp)[r] = make_uint4(q[4 * r], q[4 * r + 1], q[4 * r + 2], q[4 * r + 3]);
 			} else {
 #pragma unroll
-				for (uint32_t j = 0; j < AIRS_PT; j++)
+				for (uint32_t j = 0; j < EPT; j++)
 					if (okmask & (1u << j))
 						mpp[j] = (uint16_t)(nmp[0][j >> 1] >> (16u * (j & 1u)));
 			}
@@ -1141,7 +1168,7 @@ __global__ __launch_bounds__(AIRS_WG) void encode_kernel(KArgs a)
 #pragma unroll
 		for (uint32_t k = 0; k + 1 < CH; k++) {
 #pragma unroll
-			for (uint32_t i = 0; i < AIRS_PT / 2; i++) {
+			for (uint32_t i = 0; i < EPT / 2; i++) {
 				mp[k][i] = mp[k + 1][i];
 				if (AIRS_KEEP_Q)
 					mq[AIRS_KEEP_Q ? k : 0][i] = mq[AIRS_KEEP_Q ? k + 1 : 0][i];
@@ -1270,6 +1297,53 @@ __device__ __forceinline__ int16_t iwt_sample(const uint8_t *fsrc, uint32_t i)
 
 // whole frame in LDS (n <= AIRS_IWT_LDS_MAX): one 1024-thread workgroup per frame
 #define AIRS_IWT_LDS_MAX 65536u
+// LDS view of a frame with a bank swizzle: element i lives in 32-bit word
+// w ^ ((w >> 5) & 31), w = i / 2, so the stride-2s accesses of a level spread
+// over the LDS banks instead of piling onto one
+struct IwtLds {
+	int16_t *base;
+	__device__ __forceinline__ int16_t &operator[](uint64_t i) const
+	{
+		const uint32_t w = (uint32_t)i >> 1;
+		return base[2u * (w ^ ((w >> 5) & 31u)) + ((uint32_t)i & 1u)];
+	}
+};
+
+// one phase of level s in LDS: the odd (ODD) or even coefficients, four items
+// per thread per round with all their operands loaded before any store (a
+// phase never reads what it writes, except each item its own slot)
+template <bool ODD>
+__device__ __forceinline__ void iwt_phase_lds(const IwtLds &y, uint32_t n, uint32_t s, uint32_t tid)
+{
+	const uint32_t cnt = ODD ? (n > s ? (n - s + 2u * s - 1u) / (2u * s) : 0u) : (n + 2u * s - 1u) / (2u * s);
+	for (uint32_t b0 = 0; b0 < cnt; b0 += 4u * 1024u) {
+		int32_t c[4], l[4], r[4];
+		uint32_t idx[4];
+		// neighbour indices clamped into the frame (a missing neighbour reads
+		// the item itself and is not used), so every load is unconditional
+#pragma unroll
+		for (uint32_t u = 0; u < 4; u++) {
+			const uint32_t t = min(b0 + u * 1024u + tid, cnt - 1u);
+			const uint32_t i = ODD ? s + 2u * s * t : 2u * s * t;
+			idx[u] = i;
+			c[u] = y[i];
+			l[u] = y[i >= s ? i - s : i];
+			r[u] = y[i + s < n ? i + s : i];
+		}
+#pragma unroll
+		for (uint32_t u = 0; u < 4; u++) {
+			const uint32_t i = idx[u];
+			int16_t v;
+			if (ODD)
+				v = i + s < n ? iwt_odd(c[u], l[u], r[u]) : (int16_t)(c[u] - l[u]);
+			else
+				v = i == 0 ? iwt_edge(c[u], r[u]) : i + s < n ? iwt_even(c[u], l[u], r[u]) : iwt_edge(c[u], l[u]);
+			if (b0 + u * 1024u + tid < cnt)
+				y[i] = v;
+		}
+	}
+}
+
 template <int W>
 __global__ __launch_bounds__(1024) void iwt_frame_kernel(IwtArgs a)
 {
@@ -1278,17 +1352,128 @@ __global__ __launch_bounds__(1024) void iwt_frame_kernel(IwtArgs a)
 	int16_t *coef = iwt_frame_coef(a, blockIdx.x, &frame);
 	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
 	const uint32_t n = a.n, tid = threadIdx.x;
-	for (uint32_t i = tid; i < n; i += 1024u)
-		L_iwt[i] = iwt_sample<W>(fsrc, i);
+	const IwtLds y{L_iwt};
+	// samples -> LDS: 16-byte loads when the frame is 16-byte aligned
+	uint32_t done = 0;
+	if (((uintptr_t)fsrc & 15u) == 0) {
+		constexpr uint32_t PER = 16u / W; // samples per 16-byte load
+		const uint32_t nq = n / PER;
+		for (uint32_t q = tid; q < nq; q += 1024u) {
+			const uint4 v = reinterpret_cast<const uint4 *>(fsrc)[q];
+			const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+			for (uint32_t e = 0; e < 4; e++) {
+				if (W == 2) {
+					y[PER * q + 2u * e] = (int16_t)(vw[e] & 0xFFFFu);
+					y[PER * q + 2u * e + 1u] = (int16_t)(vw[e] >> 16);
+				} else {
+					y[PER * q + e] = (int16_t)(vw[e] & 0xFFFFu);
+				}
+			}
+		}
+		done = nq * PER;
+	}
+	for (uint32_t i = done + tid; i < n; i += 1024u)
+		y[i] = iwt_sample<W>(fsrc, i);
 	__syncthreads();
-	for (uint32_t s = 1; s < n; s <<= 1) {
-		iwt_odds(L_iwt, n, s, tid, 1024u);
+#ifndef AIRS_IWT_ABL
+#define AIRS_IWT_ABL 0
+#endif
+	for (uint32_t s = 1; s < (AIRS_IWT_ABL ? 0u : n); s <<= 1) {
+		iwt_phase_lds<true>(y, n, s, tid);
 		__syncthreads();
-		iwt_evens(L_iwt, n, s, tid, 1024u);
+		iwt_phase_lds<false>(y, n, s, tid);
 		__syncthreads();
 	}
-	for (uint32_t i = tid; i < n; i += 1024u)
-		coef[i] = L_iwt[i];
+	// LDS -> work buffer: two coefficients per 32-bit store when aligned
+	if (((uintptr_t)coef & 3u) == 0) {
+		uint32_t *c32 = reinterpret_cast<uint32_t *>(coef);
+		for (uint32_t q = tid; q < n / 2u; q += 1024u)
+			c32[q] = (uint32_t)(uint16_t)y[2u * q] | ((uint32_t)(uint16_t)y[2u * q + 1u] << 16);
+		if ((n & 1u) && tid == 0)
+			coef[n - 1u] = y[n - 1u];
+	} else {
+		for (uint32_t i = tid; i < n; i += 1024u)
+			coef[i] = y[i];
+	}
+}
+
+// Frames of 64 k samples (n a multiple of 64, n <= 65536): thread t holds
+// samples [64t, 64t + 64) in registers and runs the six levels s = 1 .. 32
+// there; per level it needs the next block's first sample (odd phase) and
+// the previous block's last odd coefficient (even phase), swapped through
+// LDS.  The remaining levels (strides 64, 128, ...) act on the n / 64 block
+// heads, which the LDS phases handle as a frame of their own.
+template <int W>
+__global__ __launch_bounds__(1024) void iwt_block_kernel(IwtArgs a)
+{
+	__shared__ int16_t h_first[1024], h_odd[1024], heads[1024 + 64];
+	uint32_t frame;
+	int16_t *coef = iwt_frame_coef(a, blockIdx.x, &frame);
+	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
+	const uint32_t n = a.n, nb = n / 64u, t = threadIdx.x;
+	const bool act = t < nb, last = t + 1u == nb;
+	int32_t x[64];
+	if (act) {
+		const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)t * 64u * W);
+#pragma unroll
+		for (uint32_t q = 0; q < 64u * W / 16u; q++) {
+			const uint4 v = p[q];
+			const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+			for (uint32_t e = 0; e < 4; e++) {
+				if (W == 2) {
+					x[8 * q + 2 * e] = (int16_t)(vw[e] & 0xFFFFu);
+					x[8 * q + 2 * e + 1] = (int16_t)(vw[e] >> 16);
+				} else {
+					x[4 * q + e] = (int16_t)(vw[e] & 0xFFFFu);
+				}
+			}
+		}
+	}
+#pragma unroll
+	for (uint32_t s = 1; s < 64u; s <<= 1) {
+		if (act)
+			h_first[t] = (int16_t)x[0];
+		__syncthreads();
+		const int32_t rh = act && !last ? h_first[t + 1u] : 0;
+#pragma unroll
+		for (uint32_t k = s; k < 64u; k += 2u * s) {
+			if (k + s < 64u)
+				x[k] = iwt_odd(x[k], x[k - s], x[k + s]);
+			else // the block's last odd: its right neighbour is the next block's head
+				x[k] = last ? (int16_t)(x[k] - x[k - s]) : iwt_odd(x[k], x[k - s], rh);
+		}
+		if (act)
+			h_odd[t] = (int16_t)x[64u - s];
+		__syncthreads();
+		const int32_t lh = act && t ? h_odd[t - 1u] : 0;
+		x[0] = t ? iwt_even(x[0], lh, x[s]) : iwt_edge(x[0], x[s]);
+#pragma unroll
+		for (uint32_t k = 2u * s; k < 64u; k += 2u * s)
+			x[k] = iwt_even(x[k], x[k - s], x[k + s]);
+	}
+	// strides 64, 128, ...: the block heads as a frame of nb samples
+	const IwtLds y{heads};
+	if (act)
+		y[t] = (int16_t)x[0];
+	__syncthreads();
+	for (uint32_t s = 1; s < nb; s <<= 1) {
+		iwt_phase_lds<true>(y, nb, s, t);
+		__syncthreads();
+		iwt_phase_lds<false>(y, nb, s, t);
+		__syncthreads();
+	}
+	if (act) {
+		x[0] = y[t];
+		uint4 *o = reinterpret_cast<uint4 *>(coef + (size_t)t * 64u);
+#pragma unroll
+		for (uint32_t q = 0; q < 8u; q++)
+			o[q] = make_uint4((uint32_t)(uint16_t)x[8 * q] | ((uint32_t)(uint16_t)x[8 * q + 1] << 16),
+					  (uint32_t)(uint16_t)x[8 * q + 2] | ((uint32_t)(uint16_t)x[8 * q + 3] << 16),
+					  (uint32_t)(uint16_t)x[8 * q + 4] | ((uint32_t)(uint16_t)x[8 * q + 5] << 16),
+					  (uint32_t)(uint16_t)x[8 * q + 6] | ((uint32_t)(uint16_t)x[8 * q + 7] << 16));
+	}
 }
 
 // larger frames: samples -> work buffer, then two launches per level
@@ -1644,14 +1829,14 @@ static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t 
 		return;
 	} else {
 		if (full)
-			hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true>), dim3(grid), dim3(AIRS_WG), lds, s, k);
+			hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true>), dim3(grid), dim3(EWG), lds, s, k);
 		return;
 	}
 #else
 	if (full)
-		hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true>), dim3(grid), dim3(AIRS_WG), lds, s, k);
+		hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true>), dim3(grid), dim3(EWG), lds, s, k);
 	else
-		hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, false>), dim3(grid), dim3(AIRS_WG), lds, s, k);
+		hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, false>), dim3(grid), dim3(EWG), lds, s, k);
 #endif
 }
 
@@ -1718,6 +1903,19 @@ static uint32_t run_iwt(struct airs_dev_engine *e, const struct airs_launch *L)
 	a.frame_mul = L->frame_list ? 0u : L->frame_mul;
 	a.n = L->n;
 	const bool w2 = L->sample_bytes == 2;
+	// whole 64-sample blocks, 16-byte aligned frames and work buffers: the
+	// register kernel
+	const bool al = ((uintptr_t)L->src & 15u) == 0 && (L->src_stride & 15u) == 0 &&
+			(L->model_ptrs ? L->model_ptrs_al16 != 0u
+				       : ((uintptr_t)L->model & 15u) == 0 && (L->model_stride & 15u) == 0);
+	if (L->n % 64u == 0 && L->n >= 128u && L->n <= 65536u && al) {
+		if (w2)
+			hipLaunchKernelGGL(iwt_block_kernel<2>, dim3(L->num_frames), dim3(1024), 0, e->stream, a);
+		else
+			hipLaunchKernelGGL(iwt_block_kernel<4>, dim3(L->num_frames), dim3(1024), 0, e->stream, a);
+		HIPCHECK(hipGetLastError());
+		return 0;
+	}
 	if (L->n <= AIRS_IWT_LDS_MAX) {
 		static bool attr = false;
 		if (!attr) {
@@ -1728,7 +1926,7 @@ static uint32_t run_iwt(struct airs_dev_engine *e, const struct airs_launch *L)
 						     hipFuncAttributeMaxDynamicSharedMemorySize, mx));
 			attr = true;
 		}
-		const size_t lds = (size_t)L->n * 2u;
+		const size_t lds = (size_t)((L->n + 63u) & ~63u) * 2u; // whole swizzle blocks
 		if (w2)
 			hipLaunchKernelGGL(iwt_frame_kernel<2>, dim3(L->num_frames), dim3(1024), lds, e->stream, a);
 		else
