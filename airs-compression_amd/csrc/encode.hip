@@ -1279,6 +1279,7 @@ struct IwtArgs {
 	const uint32_t *frame_list;
 	uint32_t frame_add, frame_mul, coef_div;
 	uint32_t n;
+	int16_t *heads; // two-phase kernels: launch frame j's block heads at heads + j * n / 64
 };
 
 __device__ __forceinline__ int16_t *iwt_frame_coef(const IwtArgs &a, uint32_t j, uint32_t *frame)
@@ -1312,18 +1313,18 @@ struct IwtLds {
 // one phase of level s in LDS: the odd (ODD) or even coefficients, four items
 // per thread per round with all their operands loaded before any store (a
 // phase never reads what it writes, except each item its own slot)
-template <bool ODD>
+template <bool ODD, uint32_t NT = 1024u>
 __device__ __forceinline__ void iwt_phase_lds(const IwtLds &y, uint32_t n, uint32_t s, uint32_t tid)
 {
 	const uint32_t cnt = ODD ? (n > s ? (n - s + 2u * s - 1u) / (2u * s) : 0u) : (n + 2u * s - 1u) / (2u * s);
-	for (uint32_t b0 = 0; b0 < cnt; b0 += 4u * 1024u) {
+	for (uint32_t b0 = 0; b0 < cnt; b0 += 4u * NT) {
 		int32_t c[4], l[4], r[4];
 		uint32_t idx[4];
 		// neighbour indices clamped into the frame (a missing neighbour reads
 		// the item itself and is not used), so every load is unconditional
 #pragma unroll
 		for (uint32_t u = 0; u < 4; u++) {
-			const uint32_t t = min(b0 + u * 1024u + tid, cnt - 1u);
+			const uint32_t t = min(b0 + u * NT + tid, cnt - 1u);
 			const uint32_t i = ODD ? s + 2u * s * t : 2u * s * t;
 			idx[u] = i;
 			c[u] = y[i];
@@ -1338,7 +1339,7 @@ __device__ __forceinline__ void iwt_phase_lds(const IwtLds &y, uint32_t n, uint3
 				v = i + s < n ? iwt_odd(c[u], l[u], r[u]) : (int16_t)(c[u] - l[u]);
 			else
 				v = i == 0 ? iwt_edge(c[u], r[u]) : i + s < n ? iwt_even(c[u], l[u], r[u]) : iwt_edge(c[u], l[u]);
-			if (b0 + u * 1024u + tid < cnt)
+			if (b0 + u * NT + tid < cnt)
 				y[i] = v;
 		}
 	}
@@ -1474,6 +1475,103 @@ __global__ __launch_bounds__(1024) void iwt_block_kernel(IwtArgs a)
 					  (uint32_t)(uint16_t)x[8 * q + 4] | ((uint32_t)(uint16_t)x[8 * q + 5] << 16),
 					  (uint32_t)(uint16_t)x[8 * q + 6] | ((uint32_t)(uint16_t)x[8 * q + 7] << 16));
 	}
+}
+
+// Frames of any size with n a multiple of 64 (n >= 128), in two launches.
+// Phase A: a 256-thread workgroup takes IWT_RB = 252 consecutive 64-sample
+// blocks of a frame plus two halo blocks on each side (the dependency cone of
+// six levels is under 128 samples), runs levels s = 1 .. 32 in registers as
+// iwt_block_kernel does, and writes its real blocks (their heads still at
+// level 6).  Phase B: one workgroup per frame runs the levels s >= 64 on the
+// n / 64 heads in LDS and writes them back.
+#define IWT_RB 252u
+template <int W>
+__global__ __launch_bounds__(256) void iwt_blocks_a_kernel(IwtArgs a, uint32_t wg_per_frame)
+{
+	__shared__ int16_t h_first[256], h_odd[256];
+	const uint32_t j = blockIdx.x / wg_per_frame, part = blockIdx.x - j * wg_per_frame;
+	uint32_t frame;
+	int16_t *coef = iwt_frame_coef(a, j, &frame);
+	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
+	const uint32_t nb = a.n / 64u, t = threadIdx.x;
+	const int32_t gb = (int32_t)(part * IWT_RB + t) - 2; // global block of this thread
+	const bool act = gb >= 0 && gb < (int32_t)nb;
+	const bool first = gb == 0, last = gb + 1 == (int32_t)nb;
+	int32_t x[64];
+	if (act) {
+		const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)gb * 64u * W);
+#pragma unroll
+		for (uint32_t q = 0; q < 64u * W / 16u; q++) {
+			const uint4 v = p[q];
+			const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+			for (uint32_t e = 0; e < 4; e++) {
+				if (W == 2) {
+					x[8 * q + 2 * e] = (int16_t)(vw[e] & 0xFFFFu);
+					x[8 * q + 2 * e + 1] = (int16_t)(vw[e] >> 16);
+				} else {
+					x[4 * q + e] = (int16_t)(vw[e] & 0xFFFFu);
+				}
+			}
+		}
+	} else {
+#pragma unroll
+		for (uint32_t k = 0; k < 64u; k++)
+			x[k] = 0;
+	}
+#pragma unroll
+	for (uint32_t s = 1; s < 64u; s <<= 1) {
+		h_first[t] = (int16_t)x[0];
+		__syncthreads();
+		const int32_t rh = t + 1u < 256u ? h_first[t + 1u] : 0;
+#pragma unroll
+		for (uint32_t k = s; k < 64u; k += 2u * s) {
+			if (k + s < 64u)
+				x[k] = iwt_odd(x[k], x[k - s], x[k + s]);
+			else
+				x[k] = last ? (int16_t)(x[k] - x[k - s]) : iwt_odd(x[k], x[k - s], rh);
+		}
+		h_odd[t] = (int16_t)x[64u - s];
+		__syncthreads();
+		const int32_t lh = t ? h_odd[t - 1u] : 0;
+		x[0] = first ? iwt_edge(x[0], x[s]) : iwt_even(x[0], lh, x[s]);
+#pragma unroll
+		for (uint32_t k = 2u * s; k < 64u; k += 2u * s)
+			x[k] = iwt_even(x[k], x[k - s], x[k + s]);
+	}
+	if (act && t >= 2u && t < 2u + IWT_RB) {
+		a.heads[(size_t)j * nb + gb] = (int16_t)x[0];
+		uint4 *o = reinterpret_cast<uint4 *>(coef + (size_t)gb * 64u);
+#pragma unroll
+		for (uint32_t q = 0; q < 8u; q++)
+			o[q] = make_uint4((uint32_t)(uint16_t)x[8 * q] | ((uint32_t)(uint16_t)x[8 * q + 1] << 16),
+					  (uint32_t)(uint16_t)x[8 * q + 2] | ((uint32_t)(uint16_t)x[8 * q + 3] << 16),
+					  (uint32_t)(uint16_t)x[8 * q + 4] | ((uint32_t)(uint16_t)x[8 * q + 5] << 16),
+					  (uint32_t)(uint16_t)x[8 * q + 6] | ((uint32_t)(uint16_t)x[8 * q + 7] << 16));
+	}
+}
+
+// one wave per frame: the heads are few (n / 64), and a one-wave workgroup
+// pays nothing for its barriers
+__global__ __launch_bounds__(64) void iwt_heads_b_kernel(IwtArgs a)
+{
+	extern __shared__ int16_t L_heads[];
+	uint32_t frame;
+	int16_t *coef = iwt_frame_coef(a, blockIdx.x, &frame);
+	const uint32_t nb = a.n / 64u, t = threadIdx.x;
+	const IwtLds y{L_heads};
+	const int16_t *hd = a.heads + (size_t)blockIdx.x * nb;
+	for (uint32_t i = t; i < nb; i += 64u)
+		y[i] = hd[i];
+	__syncthreads();
+	for (uint32_t s = 1; s < nb; s <<= 1) {
+		iwt_phase_lds<true, 64u>(y, nb, s, t);
+		__syncthreads();
+		iwt_phase_lds<false, 64u>(y, nb, s, t);
+		__syncthreads();
+	}
+	for (uint32_t i = t; i < nb; i += 64u)
+		coef[(size_t)i * 64u] = y[i];
 }
 
 // larger frames: samples -> work buffer, then two launches per level
@@ -1903,11 +2001,37 @@ static uint32_t run_iwt(struct airs_dev_engine *e, const struct airs_launch *L)
 	a.frame_mul = L->frame_list ? 0u : L->frame_mul;
 	a.n = L->n;
 	const bool w2 = L->sample_bytes == 2;
+	static bool attr_b = false;
+	if (!attr_b) { // heads of frames up to 4 Mi samples: up to 128 KiB of LDS
+		HIPCHECK(hipFuncSetAttribute((const void *)iwt_heads_b_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+					     (int)(AIRS_IWT_LDS_MAX * 2u)));
+		attr_b = true;
+	}
 	// whole 64-sample blocks, 16-byte aligned frames and work buffers: the
 	// register kernel
 	const bool al = ((uintptr_t)L->src & 15u) == 0 && (L->src_stride & 15u) == 0 &&
 			(L->model_ptrs ? L->model_ptrs_al16 != 0u
 				       : ((uintptr_t)L->model & 15u) == 0 && (L->model_stride & 15u) == 0);
+#ifndef AIRS_IWT_TWO_PHASE
+#define AIRS_IWT_TWO_PHASE 1
+#endif
+	if (AIRS_IWT_TWO_PHASE && L->n % 64u == 0 && L->n >= 128u && L->n / 64u <= 65536u && al) {
+		const uint32_t nb = L->n / 64u, wpf = (nb + IWT_RB - 1u) / IWT_RB;
+		const uint64_t grid = (uint64_t)wpf * L->num_frames;
+		if (grid > 0x7FFFFFFFull)
+			return ERRV(E_PARAMS_INVALID);
+		a.heads = (int16_t *)airs_dev_scratch(e, AIRS_NSLOT - 1, (size_t)nb * L->num_frames * 2u);
+		if (!a.heads)
+			return ERRV(E_GENERIC);
+		if (w2)
+			hipLaunchKernelGGL(iwt_blocks_a_kernel<2>, dim3((uint32_t)grid), dim3(256), 0, e->stream, a, wpf);
+		else
+			hipLaunchKernelGGL(iwt_blocks_a_kernel<4>, dim3((uint32_t)grid), dim3(256), 0, e->stream, a, wpf);
+		const size_t lds = (size_t)((nb + 63u) & ~63u) * 2u;
+		hipLaunchKernelGGL(iwt_heads_b_kernel, dim3(L->num_frames), dim3(64), lds, e->stream, a);
+		HIPCHECK(hipGetLastError());
+		return 0;
+	}
 	if (L->n % 64u == 0 && L->n >= 128u && L->n <= 65536u && al) {
 		if (w2)
 			hipLaunchKernelGGL(iwt_block_kernel<2>, dim3(L->num_frames), dim3(1024), 0, e->stream, a);
@@ -1926,6 +2050,7 @@ static uint32_t run_iwt(struct airs_dev_engine *e, const struct airs_launch *L)
 						     hipFuncAttributeMaxDynamicSharedMemorySize, mx));
 			attr = true;
 		}
+
 		const size_t lds = (size_t)((L->n + 63u) & ~63u) * 2u; // whole swizzle blocks
 		if (w2)
 			hipLaunchKernelGGL(iwt_frame_kernel<2>, dim3(L->num_frames), dim3(1024), lds, e->stream, a);

@@ -99,7 +99,7 @@ def test_iwt_sizes_vs_oracle(gpu, orc, kind):
     the samples are encoded), and IWT as the secondary pass."""
     sb = 4 if kind == "i16_in_i32" else 2
     for n in (1, 2, 3, 4, 5, 6, 7, 9, 16, 17, 33, 64, 128, 192, 1000, 4095, 4096, 4097, 8256, 65472, 65535,
-              65536, 65537, 131075, 300001):
+              65536, 65537, 131075, 300001, 1048576 + 64):
         for prm in (dict(primary_preprocessing=2, primary_encoder_type=1, primary_encoder_param=16),
                     dict(primary_preprocessing=2, primary_encoder_type=2, primary_encoder_param=10,
                          primary_encoder_outlier=200, secondary_iterations=2, secondary_preprocessing=3,
