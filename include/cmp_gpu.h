@@ -40,9 +40,9 @@ enum cmp_gpu_sample_type {
 };
 
 /* flags */
-#define CMP_GPU_AUTO_RICE 0x1u /* GOLOMB_ZERO passes: choose g = 2^k per frame (k in [0,15],
-				* fewest payload bits, ties to smaller k) instead of the
-				* configured encoder parameter; build-defined extension */
+#define CMP_GPU_AUTO_RICE 0x1u /* GOLOMB_ZERO passes other than IWT: choose g = 2^k per frame
+				* (k in [0,15], fewest payload bits, ties to smaller k) instead
+				* of the configured encoder parameter; build-defined extension */
 
 struct cmp_gpu_batch {
 	enum cmp_gpu_sample_type type;
