@@ -1640,7 +1640,23 @@ __global__ __launch_bounds__(64) void checksum_kernel(const uint8_t *src, uint64
 	const uint32_t len = 2u * n;
 	const uint32_t stripes = len >= 16u ? n / 8u : 0u;
 	uint32_t acc = q == 0 ? seed + XP1 + XP2 : q == 1 ? seed + XP2 : q == 2 ? seed : seed - XP1;
-	for (uint32_t s = 0; s < stripes; s++) {
+	// The accumulator chain is serial (xxhash round: acc = rotl(acc + x P2, 13) P1),
+	// so the loads of a batch of 16 stripes are issued before its 16 rounds and
+	// x P2 is computed off the chain: the chain is then add, rotate, multiply.
+	uint32_t s = 0;
+	if (W == 2 && ((uintptr_t)f & 3u) == 0) { // lane q's 4 bytes of a stripe are one aligned dword
+		const uint32_t *f32 = reinterpret_cast<const uint32_t *>(f);
+		for (; s + 16u <= stripes; s += 16u) {
+			uint32_t xv[16];
+#pragma unroll
+			for (uint32_t u = 0; u < 16u; u++)
+				xv[u] = __builtin_amdgcn_perm(f32[4u * (s + u) + q], f32[4u * (s + u) + q], 0x02030001u) * XP2;
+#pragma unroll
+			for (uint32_t u = 0; u < 16u; u++)
+				acc = rotl32(acc + xv[u], 13) * XP1;
+		}
+	}
+	for (; s < stripes; s++) {
 		const uint32_t i = 8u * s + 2u * q;
 		acc = rotl32(acc + be_pair(sample_at<W>(f, i), sample_at<W>(f, i + 1u)) * XP2, 13) * XP1;
 	}
