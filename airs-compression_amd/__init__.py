@@ -68,6 +68,20 @@ class GpuBatch(ctypes.Structure):
     ]
 
 
+class GpuDecodeBatch(ctypes.Structure):
+    """struct cmp_gpu_decode_batch (include/cmp_gpu.h)."""
+    _fields_ = [
+        ("src", c_void_p),
+        ("src_stride", c_uint64),
+        ("src_capacity", c_uint32),
+        ("num_frames", c_uint32),
+        ("dst", c_void_p),
+        ("dst_stride", c_uint64),
+        ("dst_samples", c_uint32),
+        ("status", c_void_p),
+    ]
+
+
 class AirsLib(CmpLib):
     """CmpLib plus the cmp_gpu.h device batch API."""
 
@@ -86,6 +100,8 @@ class AirsLib(CmpLib):
         L.cmp_gpu_synthesize.argtypes = [c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_uint32,
                                          c_uint32, c_uint64, c_uint32]
         L.cmp_gpu_synthesize.restype = c_uint32
+        L.cmp_gpu_decompress.argtypes = [c_void_p, POINTER(GpuDecodeBatch)]
+        L.cmp_gpu_decompress.restype = c_uint32
 
     def gpu_available(self) -> bool:
         return bool(self.lib.cmp_gpu_available())
@@ -125,6 +141,13 @@ class GpuEngine:
                      sizes=sizes_ptr, flags=flags)
         n_ctx = len(ctxs)
         return self.lib.lib.cmp_gpu_compress(self.handle, ctxs, n_ctx, frames_per_ctx, ctypes.byref(b))
+
+    def decompress(self, src_ptr: int, src_stride: int, src_capacity: int, num_frames: int, dst_ptr: int,
+                   dst_stride: int, dst_samples: int, status_ptr: int) -> int:
+        """cmp_gpu_decompress over device pointers (frames -> 16-bit samples)."""
+        b = GpuDecodeBatch(src=src_ptr, src_stride=src_stride, src_capacity=src_capacity, num_frames=num_frames,
+                           dst=dst_ptr, dst_stride=dst_stride, dst_samples=dst_samples, status=status_ptr)
+        return self.lib.lib.cmp_gpu_decompress(self.handle, ctypes.byref(b))
 
     def synchronize(self) -> int:
         return self.lib.lib.cmp_gpu_synchronize(self.handle)

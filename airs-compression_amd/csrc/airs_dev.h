@@ -100,7 +100,8 @@ uint32_t airs_dev_synth(struct airs_dev_engine *e, void *dst, uint32_t sample_by
 			uint32_t W);
 
 /* engine-owned scratch, grown on demand (stream ordered) */
-#define AIRS_NSLOT 12 /* scratch slots per engine; the last one is the device layer's (IWT heads) */
+#define AIRS_NSLOT 12 /* scratch slots per engine; the last three are the device layer's
+		       * (decoder parse arrays, decoder frame info, IWT heads) */
 void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes);
 
 /* rewrite header bytes 8..13 (identifier) of launch frames whose status is
@@ -108,6 +109,12 @@ void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes);
 uint32_t airs_dev_patch_ids(struct airs_dev_engine *e, void *dst, uint64_t dst_stride, uint32_t num_frames,
 			    uint32_t frame_add, uint32_t frame_mul, const uint64_t *ids,
 			    const uint32_t *status);
+
+/* decoder (decode.hip): frames at src + f*src_stride -> 16-bit samples at
+ * dst + f*dst_stride bytes; status[f] = samples or error (see cmp_gpu.h) */
+uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, uint64_t src_stride, uint32_t src_cap,
+			 uint32_t num_frames, uint16_t *dst, uint64_t dst_stride, uint32_t dst_samples,
+			 uint32_t *status);
 
 /* plain memory helpers on the engine stream */
 void *airs_dev_malloc(size_t bytes);

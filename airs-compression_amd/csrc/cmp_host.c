@@ -556,6 +556,17 @@ struct cmp_gpu_engine {
 	struct airs_dev_engine *dev;
 };
 
+uint32_t cmp_gpu_decompress(struct cmp_gpu_engine *engine, const struct cmp_gpu_decode_batch *b)
+{
+	if (!engine || !b || !b->src || !b->dst || !b->status || !b->num_frames || b->num_frames > 65535u)
+		return ERRV(GENERIC);
+	if (((uintptr_t)b->src & 7u) || (b->src_stride & 7u) || b->src_capacity < HDR_MAX_SIZE ||
+	    (b->src_capacity & 3u) || (b->num_frames > 1 && b->src_stride < b->src_capacity))
+		return ERRV(GENERIC);
+	return airs_dev_decode(engine->dev, b->src, b->src_stride, b->src_capacity, b->num_frames, b->dst,
+			       b->dst_stride, b->dst_samples, b->status);
+}
+
 int cmp_gpu_available(void)
 {
 	return airs_dev_available();

@@ -78,6 +78,28 @@ void cmp_gpu_engine_destroy(struct cmp_gpu_engine *engine);
 uint32_t cmp_gpu_compress(struct cmp_gpu_engine *engine, struct cmp_context *ctx, uint32_t num_ctx,
 			  uint32_t frames_per_ctx, const struct cmp_gpu_batch *batch);
 
+/* Decoder (no reference counterpart: the reference has none, see
+ * programs/airspacecli.c:421-423).  Decodes num_frames frames as written by
+ * cmp_compress_* / cmp_gpu_compress back into their 16-bit samples (the low
+ * halves, for i16-in-i32 sources).  Frames with NONE or DIFF preprocessing and
+ * any encoder; MODEL and IWT frames get CMP_ERR_PARAMS_INVALID.  The checksum
+ * is not verified. */
+struct cmp_gpu_decode_batch {
+	const void *src;        /* device; frame i at src + i*src_stride, 8-byte aligned */
+	uint64_t src_stride;    /* bytes, multiple of 8, >= src_capacity */
+	uint32_t src_capacity;  /* bytes readable per frame, multiple of 4, >= 22 */
+	uint32_t num_frames;    /* <= 65535 */
+	uint16_t *dst;          /* device; frame i's samples at dst + i*dst_stride bytes */
+	uint64_t dst_stride;    /* bytes, even */
+	uint32_t dst_samples;   /* samples available per frame */
+	uint32_t *status;       /* device [num_frames]: samples decoded, or an error value */
+};
+
+/* Returns CMP_ERR_NO_ERROR or a call-level error; per-frame results land in
+ * batch->status.  Synchronises with the host (the parse is sized from the
+ * headers and repeated until it settles). */
+uint32_t cmp_gpu_decompress(struct cmp_gpu_engine *engine, const struct cmp_gpu_decode_batch *batch);
+
 /* wait for all work queued on the engine */
 uint32_t cmp_gpu_synchronize(struct cmp_gpu_engine *engine);
 

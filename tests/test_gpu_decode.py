@@ -1,0 +1,127 @@
+"""GPU decoder (cmp_gpu_decompress).  The reference has
+no decoder, so parity is anchored on the encoder: frames written by the CPU
+oracle's encoder must decode to the samples it encoded (and to what the
+oracle's own decoder, orc_decode, returns), and frames written by the GPU
+encoder must round-trip at BASELINE sizes.  Bit-exact (16-bit samples)."""
+import numpy as np
+import pytest
+
+import configs
+import scenarios
+from conftest import load_pkg
+
+pytestmark = pytest.mark.gpu
+api = load_pkg().cmpapi
+
+
+@pytest.fixture(scope="module")
+def gpu(prod):
+    if not prod.gpu_available():
+        pytest.fail("GPU test run without a usable HIP device")
+    return prod
+
+
+@pytest.fixture(scope="module")
+def eng(gpu):
+    e = gpu.engine()
+    yield e
+    e.close()
+
+
+def gpu_decode(eng, frames, n_max, cap=None):
+    """Upload frames (bytes) at a common stride, decode on the GPU; returns
+    (status list, samples per frame as uint16 arrays)."""
+    import torch
+    cap = cap or max(22, max(len(f) for f in frames))
+    cap = (cap + 7) // 8 * 8
+    nf = len(frames)
+    host = np.zeros(nf * cap, dtype=np.uint8)
+    for i, f in enumerate(frames):
+        host[i * cap:i * cap + len(f)] = np.frombuffer(f, dtype=np.uint8)
+    src = torch.from_numpy(host).cuda()
+    dstride = 2 * max(n_max, 1)
+    dst = torch.zeros(nf * dstride // 2, dtype=torch.int16, device="cuda")
+    st = torch.zeros(nf, dtype=torch.int32, device="cuda")
+    assert eng.decompress(src.data_ptr(), cap, cap, nf, dst.data_ptr(), dstride, n_max, st.data_ptr()) == 0
+    assert eng.synchronize() == 0
+    status = [int(s) & 0xFFFFFFFF for s in st.cpu().numpy()]
+    out = dst.cpu().numpy().view(np.uint16)
+    return status, [out[i * (dstride // 2):(i + 1) * (dstride // 2)] for i in range(nf)]
+
+
+def oracle_frame(orc, params, kind, x):
+    ctx = api.CmpContext()
+    assert not api.is_error(orc.initialise(ctx, params))
+    cap = 26 + 6 * len(x) + 64
+    dst = api.aligned_empty(cap)
+    r = orc.compress(kind, ctx, dst, cap, x)
+    assert not api.is_error(r), api.error_name(r)
+    return bytes(dst[:r])
+
+
+def test_decode_vs_oracle_frames(eng, orc, orc_ext):
+    """Random NONE / DIFF frames of every encoder, Golomb parameters from 1 to
+    65535 (Rice and general), outliers, checksums, sizes from 1 to 70 k."""
+    import random
+    rng = random.Random(11)
+    frames, want = [], []
+    for trial in range(160):
+        kind = rng.choice(scenarios.KINDS)
+        n = rng.choice([1, 2, 3, 7, 100, 333, 2048, 4097, 9000, 70001])
+        enc = rng.choice([0, 1, 2])
+        p = api.CmpParams(primary_preprocessing=rng.choice([0, 1]), primary_encoder_type=enc,
+                          primary_encoder_param=rng.choice([1, 2, 3, 7, 8, 10, 32, 100, 1055, 4096, 65535]),
+                          primary_encoder_outlier=rng.choice([1, 5, 107, 1000, 2**32 - 1]),
+                          checksum_enabled=rng.choice([0, 1]))
+        x = scenarios.make_src(kind, n, rng, rng.choice([1, 50, 3000, 30000]))
+        fr = oracle_frame(orc, p, kind, x)
+        out = np.zeros(n, dtype=np.uint16)
+        assert orc_ext.orc_decode(np.frombuffer(fr, dtype=np.uint8).ctypes.data, len(fr), None,
+                                  out.ctypes.data, n) == n
+        assert np.array_equal(out, (np.asarray(x).astype(np.int64) & 0xFFFF).astype(np.uint16))
+        frames.append(fr)
+        want.append(out)
+    status, outs = gpu_decode(eng, frames, 70001)
+    for i, (s, w) in enumerate(zip(status, want)):
+        assert s == len(w), (i, api.error_name(s) if api.is_error(s) else s)
+        assert np.array_equal(outs[i][:len(w)], w), i
+
+
+@pytest.mark.parametrize("name", ["cfg2_64Mi", "cfg4_8192"])
+def test_decode_roundtrip_gpu_frames(gpu, eng, orc_ext, name):
+    """Size-independent property at BASELINE size: decode(encode(x)) == x for
+    every frame the GPU encoder wrote (cfg4: the first 1024 frames)."""
+    import torch
+    cfg = dict(configs.CONFIGS[name])
+    if name == "cfg4_8192":
+        cfg["nctx"], cfg["fpc"] = 1, 1024
+    frames, _, _ = configs.gpu_frames(gpu, eng, cfg)
+    n = cfg["n"]
+    status, outs = gpu_decode(eng, frames, n)
+    assert status == [n] * len(frames)
+    src = torch.empty(len(frames) * 2 * n, dtype=torch.uint8, device="cuda")
+    assert eng.synthesize(src.data_ptr(), 2, cfg["seed"], 0, n, len(frames), 2 * n, cfg["W"]) == 0
+    x = src.cpu().numpy().view(np.uint16).reshape(len(frames), n)
+    for i in range(len(frames)):
+        assert np.array_equal(outs[i][:n], x[i]), i
+
+
+def test_decode_rejects(eng, orc):
+    """Frames the decoder does not take or cannot parse: MODEL / IWT
+    preprocessing, a broken header, a truncated payload."""
+    rng = np.random.default_rng(3)
+    x = (np.cumsum(rng.integers(-50, 50, 5000)) & 0xFFFF).astype(np.uint16)
+    good = oracle_frame(orc, api.CmpParams(primary_preprocessing=1, primary_encoder_type=1,
+                                           primary_encoder_param=16), "u16", x)
+    bad_hdr = bytearray(good)
+    bad_hdr[1] ^= 0x55  # version id
+    trunc = bytearray(good[:200])  # keep the header's sizes, cut the payload
+    trunc[2:5] = (200).to_bytes(3, "big")
+    model = bytearray(good)
+    model[15] = (3 << 4) | (model[15] & 0x0F)  # MODEL preprocessing: needs the model, not decoded
+    frames = [good, bytes(bad_hdr), bytes(trunc), bytes(model)]
+    status, outs = gpu_decode(eng, frames, 5000, cap=len(good) + 8)
+    assert status[0] == 5000 and np.array_equal(outs[0][:5000], x)
+    assert api.error_name(status[1]) == "INT_HDR"
+    assert api.error_name(status[2]) == "INT_BITSTREAM"
+    assert api.error_name(status[3]) == "PARAMS_INVALID"
