@@ -76,11 +76,10 @@ __device__ __forceinline__ uint64_t win64(const uint32_t *f32, uint32_t wmax, ui
 	return o ? (hi << o) | (d2 >> (32u - o)) : hi;
 }
 
-// one codeword at payload bit p: returns its length (0 = invalid) and m, the
-// mapped value (UNCOMPRESSED: the raw 16 bits)
-__device__ __forceinline__ uint32_t dec_symbol(const DecInfo &I, const uint32_t *f32, uint32_t p, uint32_t &m)
+// one codeword at the top of the 64-bit window W: returns its length (0 =
+// invalid) and m, the mapped value (UNCOMPRESSED: the raw 16 bits)
+__device__ __forceinline__ uint32_t dec_window(const DecInfo &I, uint64_t W, uint32_t &m)
 {
-	const uint64_t W = win64(f32, I.wmax, I.hdr_bits + p);
 	if (I.enc == 0u) { // UNCOMPRESSED (encoder.c:331-333)
 		m = (uint32_t)(W >> 48);
 		return 16u;
@@ -120,6 +119,53 @@ __device__ __forceinline__ uint32_t dec_symbol(const DecInfo &I, const uint32_t 
 	}
 	return len > 48u ? 0u : len;
 }
+
+__device__ __forceinline__ uint32_t dec_symbol(const DecInfo &I, const uint32_t *f32, uint32_t p, uint32_t &m)
+{
+	return dec_window(I, win64(f32, I.wmax, I.hdr_bits + p), m);
+}
+
+// Sequential bit reader: the next stream bits MSB-aligned in buf (nv valid,
+// zeros below), refilled a dword at a time, so a codeword costs a load only
+// every few symbols.  A codeword that does not fit the valid bits (its
+// decoded length exceeds nv: any bit it used past them was a fill zero) is
+// decoded again from memory.
+struct BitReader {
+	const uint32_t *f32;
+	uint32_t wmax, w, nv, p; // next dword, valid bits, payload bit position
+	uint64_t buf;
+	__device__ __forceinline__ void init(const DecInfo &I, const uint32_t *f, uint32_t pos)
+	{
+		f32 = f;
+		wmax = I.wmax;
+		p = pos;
+		const uint32_t abit = I.hdr_bits + pos, w0 = abit >> 5, o = abit & 31u;
+		const uint64_t hi = ((uint64_t)bswap32(f32[min(w0, wmax)]) << 32) | bswap32(f32[min(w0 + 1u, wmax)]);
+		buf = hi << o;
+		nv = 64u - o;
+		w = w0 + 2u;
+	}
+	__device__ __forceinline__ uint32_t next(const DecInfo &I, uint32_t &m)
+	{
+		if (nv <= 32u) {
+			buf |= (uint64_t)bswap32(f32[min(w, wmax)]) << (32u - nv);
+			w++;
+			nv += 32u;
+		}
+		uint32_t len = dec_window(I, buf, m);
+		if (len > nv || !len) {
+			len = dec_symbol(I, f32, p, m); // slow path: straight from memory
+			if (!len)
+				return 0u;
+			init(I, f32, p + len);
+			return len;
+		}
+		buf = len < 64u ? buf << len : 0u;
+		nv -= len;
+		p += len;
+		return len;
+	}
+};
 
 // header of every frame (header.c:24-67) -> DecInfo; NONE / DIFF frames only
 __global__ void dec_hdr_kernel(DecArgs a)
@@ -195,9 +241,11 @@ __global__ __launch_bounds__(256) void dec_parse_kernel(DecArgs a, const uint32_
 	if (start != DEC_BAD) {
 		const uint32_t *f32 = reinterpret_cast<const uint32_t *>(a.src + (uint64_t)f * a.src_stride);
 		const uint32_t end = min((s + 1u) * DEC_B, I.nbits);
+		BitReader br;
+		br.init(I, f32, start);
 		while (p < end) {
 			uint32_t m;
-			const uint32_t len = dec_symbol(I, f32, p, m);
+			const uint32_t len = br.next(I, m);
 			if (!len) {
 				p = DEC_BAD;
 				break;
@@ -261,17 +309,50 @@ __global__ __launch_bounds__(256) void dec_out_kernel(DecArgs a, const uint32_t 
 	if (s >= I.nsub || I.status)
 		return;
 	const size_t o = (size_t)f * a.msub + s;
-	uint32_t p = s ? exits[o - 1u] : 0u, j = a.base[o];
+	const uint32_t b0 = a.base[o];
+	uint32_t p = s ? exits[o - 1u] : 0u, j = b0;
 	const uint32_t end = min((s + 1u) * DEC_B, I.nbits);
 	const uint32_t *f32 = reinterpret_cast<const uint32_t *>(a.src + (uint64_t)f * a.src_stride);
 	uint16_t *out = a.dst + (uint64_t)f * (a.dst_stride / 2u);
+	// samples are shifted into a 128-bit register and leave as 16-byte stores
+	// of 8 (their run is contiguous; each lane's run starts anywhere), with
+	// 2-byte stores for the unaligned ends
+	const bool vec = (((uintptr_t)out | a.dst_stride) & 15u) == 0;
+	uint64_t lo = 0, hi = 0;
+	BitReader br;
+	if (p < end)
+		br.init(I, f32, p);
 	while (p < end && j < I.n) {
 		uint32_t m;
-		const uint32_t len = dec_symbol(I, f32, p, m);
+		const uint32_t len = br.next(I, m);
 		if (!len)
 			break;
 		p += len;
-		out[j++] = (uint16_t)(I.enc == 0u ? m : ((m >> 1) ^ (0u - (m & 1u))));
+		const uint32_t r = (I.enc == 0u ? m : ((m >> 1) ^ (0u - (m & 1u)))) & 0xFFFFu;
+		if (!vec) {
+			out[j++] = (uint16_t)r;
+			continue;
+		}
+		lo = (lo >> 16) | (hi << 48);
+		hi = (hi >> 16) | ((uint64_t)r << 48);
+		if ((j & 7u) == 7u && j - 7u >= b0) {
+			*reinterpret_cast<uint4 *>(out + (j - 7u)) =
+				make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+		} else if ((j & 7u) == 7u) {
+			// the run's first, partial group of 8: its own samples only
+			for (uint32_t i = b0; i <= j; i++) {
+				const uint32_t sh = 16u * (7u - (j - i)); // bit offset of sample i in (hi:lo)
+				out[i] = (uint16_t)(sh >= 64u ? hi >> (sh - 64u) : lo >> sh);
+			}
+		}
+		j++;
+	}
+	if (vec && (j & 7u)) { // the last, partial group
+		const uint32_t g0 = max(j & ~7u, b0);
+		for (uint32_t i = g0; i < j; i++) {
+			const uint32_t sh = 16u * (8u - (j - i)); // bit offset of sample i in (hi:lo)
+			out[i] = (uint16_t)(sh >= 64u ? hi >> (sh - 64u) : lo >> sh);
+		}
 	}
 }
 
@@ -287,8 +368,17 @@ __global__ __launch_bounds__(256) void dec_tile_sum_kernel(DecArgs a, uint32_t t
 	const uint16_t *x = a.dst + (uint64_t)f * (a.dst_stride / 2u) + (size_t)tile * DEC_TILE;
 	const uint32_t cnt = min(DEC_TILE, I.n - tile * DEC_TILE);
 	uint32_t sum = 0;
-	for (uint32_t i = t; i < cnt; i += 256u)
-		sum += x[i];
+	if (cnt == DEC_TILE && (((uintptr_t)x) & 15u) == 0) {
+		const uint4 *x4 = reinterpret_cast<const uint4 *>(x);
+		for (uint32_t q = t; q < DEC_TILE / 8u; q += 256u) {
+			const uint4 v = x4[q];
+			sum += (v.x & 0xFFFFu) + (v.x >> 16) + (v.y & 0xFFFFu) + (v.y >> 16) + (v.z & 0xFFFFu) + (v.z >> 16) +
+			       (v.w & 0xFFFFu) + (v.w >> 16);
+		}
+	} else {
+		for (uint32_t i = t; i < cnt; i += 256u)
+			sum += x[i];
+	}
 	for (uint32_t d = 32; d; d >>= 1)
 		sum += __shfl_down(sum, d, 64);
 	if ((t & 63u) == 0)
@@ -298,20 +388,41 @@ __global__ __launch_bounds__(256) void dec_tile_sum_kernel(DecArgs a, uint32_t t
 		a.tile_sum[(size_t)f * tiles + tile] = (uint16_t)(s_w[0] + s_w[1] + s_w[2] + s_w[3]);
 }
 
-__global__ void dec_tile_prefix_kernel(DecArgs a, uint32_t tiles)
+// exclusive scan of a frame's tile sums (one workgroup per frame)
+__global__ __launch_bounds__(1024) void dec_tile_prefix_kernel(DecArgs a, uint32_t tiles)
 {
-	const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-	if (f >= a.num_frames)
-		return;
+	__shared__ uint32_t s_w[16];
+	__shared__ uint32_t s_carry;
+	const uint32_t f = blockIdx.x, t = threadIdx.x, lane = t & 63u, wid = t >> 6;
 	const DecInfo I = a.info[f];
 	if (I.status || I.pre != 1u)
 		return;
-	uint16_t run = 0;
 	const uint32_t nt = (I.n + DEC_TILE - 1u) / DEC_TILE;
-	for (uint32_t t = 0; t < nt; t++) { // exclusive
-		const uint16_t v = a.tile_sum[(size_t)f * tiles + t];
-		a.tile_sum[(size_t)f * tiles + t] = run;
-		run = (uint16_t)(run + v);
+	if (t == 0)
+		s_carry = 0;
+	__syncthreads();
+	for (uint32_t b0 = 0; b0 < nt; b0 += 1024u) {
+		const uint32_t i = b0 + t;
+		uint16_t *ts = a.tile_sum + (size_t)f * tiles;
+		const uint32_t v = i < nt ? ts[i] : 0u;
+		uint32_t inc = v;
+		for (uint32_t d = 1; d < 64u; d <<= 1) {
+			const uint32_t y = __shfl_up(inc, d, 64);
+			if (lane >= d)
+				inc += y;
+		}
+		if (lane == 63u)
+			s_w[wid] = inc;
+		__syncthreads();
+		uint32_t woff = s_carry;
+		for (uint32_t w = 0; w < wid; w++)
+			woff += s_w[w];
+		if (i < nt)
+			ts[i] = (uint16_t)(woff + inc - v);
+		__syncthreads();
+		if (t == 1023u)
+			s_carry = woff + inc;
+		__syncthreads();
 	}
 }
 
@@ -326,12 +437,26 @@ __global__ __launch_bounds__(256) void dec_tile_scan_kernel(DecArgs a, uint32_t 
 	const uint32_t cnt = min(DEC_TILE, I.n - tile * DEC_TILE);
 	// thread t owns 16 consecutive samples
 	uint32_t v[16], loc = 0;
+	const bool vec = cnt == DEC_TILE && (((uintptr_t)x) & 15u) == 0;
+	if (vec) {
+		const uint4 *x4 = reinterpret_cast<const uint4 *>(x) + 2u * t;
+		const uint4 p0 = x4[0], p1 = x4[1];
+		const uint32_t w[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
 #pragma unroll
-	for (uint32_t j = 0; j < 16u; j++) {
-		const uint32_t i = 16u * t + j;
-		v[j] = i < cnt ? x[i] : 0u;
-		loc += v[j];
+		for (uint32_t q = 0; q < 8u; q++) {
+			v[2 * q] = w[q] & 0xFFFFu;
+			v[2 * q + 1] = w[q] >> 16;
+		}
+	} else {
+#pragma unroll
+		for (uint32_t j = 0; j < 16u; j++) {
+			const uint32_t i = 16u * t + j;
+			v[j] = i < cnt ? x[i] : 0u;
+		}
 	}
+#pragma unroll
+	for (uint32_t j = 0; j < 16u; j++)
+		loc += v[j];
 	uint32_t inc = loc;
 	for (uint32_t d = 1; d < 64u; d <<= 1) {
 		const uint32_t y = __shfl_up(inc, d, 64);
@@ -346,10 +471,18 @@ __global__ __launch_bounds__(256) void dec_tile_scan_kernel(DecArgs a, uint32_t 
 		run += s_w[w];
 #pragma unroll
 	for (uint32_t j = 0; j < 16u; j++) {
-		const uint32_t i = 16u * t + j;
 		run += v[j];
-		if (i < cnt)
-			x[i] = (uint16_t)run;
+		v[j] = run & 0xFFFFu;
+	}
+	if (vec) {
+		uint4 *x4 = reinterpret_cast<uint4 *>(x) + 2u * t;
+		x4[0] = make_uint4(v[0] | v[1] << 16, v[2] | v[3] << 16, v[4] | v[5] << 16, v[6] | v[7] << 16);
+		x4[1] = make_uint4(v[8] | v[9] << 16, v[10] | v[11] << 16, v[12] | v[13] << 16, v[14] | v[15] << 16);
+	} else {
+#pragma unroll
+		for (uint32_t j = 0; j < 16u; j++)
+			if (16u * t + j < cnt)
+				x[16u * t + j] = (uint16_t)v[j];
 	}
 }
 
@@ -444,7 +577,7 @@ extern "C" uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, 
 		hipLaunchKernelGGL(dec_out_kernel, grid, dim3(256), 0, s, a, (const uint32_t *)ein);
 		const dim3 tg(tiles, num_frames);
 		hipLaunchKernelGGL(dec_tile_sum_kernel, tg, dim3(256), 0, s, a, tiles);
-		hipLaunchKernelGGL(dec_tile_prefix_kernel, dim3((num_frames + 255u) / 256u), dim3(256), 0, s, a, tiles);
+		hipLaunchKernelGGL(dec_tile_prefix_kernel, dim3(num_frames), dim3(1024), 0, s, a, tiles);
 		hipLaunchKernelGGL(dec_tile_scan_kernel, tg, dim3(256), 0, s, a, tiles);
 	}
 	hipLaunchKernelGGL(dec_status_kernel, dim3((num_frames + 255u) / 256u), dim3(256), 0, s, a);
