@@ -79,6 +79,8 @@ class GpuDecodeBatch(ctypes.Structure):
         ("dst_stride", c_uint64),
         ("dst_samples", c_uint32),
         ("status", c_void_p),
+        ("model", c_void_p),
+        ("model_stride", c_uint64),
     ]
 
 
@@ -143,10 +145,12 @@ class GpuEngine:
         return self.lib.lib.cmp_gpu_compress(self.handle, ctxs, n_ctx, frames_per_ctx, ctypes.byref(b))
 
     def decompress(self, src_ptr: int, src_stride: int, src_capacity: int, num_frames: int, dst_ptr: int,
-                   dst_stride: int, dst_samples: int, status_ptr: int) -> int:
+                   dst_stride: int, dst_samples: int, status_ptr: int, model_ptr: int = 0,
+                   model_stride: int = 0) -> int:
         """cmp_gpu_decompress over device pointers (frames -> 16-bit samples)."""
         b = GpuDecodeBatch(src=src_ptr, src_stride=src_stride, src_capacity=src_capacity, num_frames=num_frames,
-                           dst=dst_ptr, dst_stride=dst_stride, dst_samples=dst_samples, status=status_ptr)
+                           dst=dst_ptr, dst_stride=dst_stride, dst_samples=dst_samples, status=status_ptr,
+                           model=model_ptr or None, model_stride=model_stride)
         return self.lib.lib.cmp_gpu_decompress(self.handle, ctypes.byref(b))
 
     def synchronize(self) -> int:

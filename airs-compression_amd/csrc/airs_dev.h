@@ -114,7 +114,7 @@ uint32_t airs_dev_patch_ids(struct airs_dev_engine *e, void *dst, uint64_t dst_s
  * dst + f*dst_stride bytes; status[f] = samples or error (see cmp_gpu.h) */
 uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, uint64_t src_stride, uint32_t src_cap,
 			 uint32_t num_frames, uint16_t *dst, uint64_t dst_stride, uint32_t dst_samples,
-			 uint32_t *status);
+			 uint32_t *status, const uint16_t *model, uint64_t model_stride);
 
 /* plain memory helpers on the engine stream */
 void *airs_dev_malloc(size_t bytes);

@@ -563,8 +563,10 @@ uint32_t cmp_gpu_decompress(struct cmp_gpu_engine *engine, const struct cmp_gpu_
 	if (((uintptr_t)b->src & 7u) || (b->src_stride & 7u) || b->src_capacity < HDR_MAX_SIZE ||
 	    (b->src_capacity & 3u) || (b->num_frames > 1 && b->src_stride < b->src_capacity))
 		return ERRV(GENERIC);
+	if (b->model && (((uintptr_t)b->model & 1u) || (b->model_stride & 1u)))
+		return ERRV(GENERIC);
 	return airs_dev_decode(engine->dev, b->src, b->src_stride, b->src_capacity, b->num_frames, b->dst,
-			       b->dst_stride, b->dst_samples, b->status);
+			       b->dst_stride, b->dst_samples, b->status, b->model, b->model_stride);
 }
 
 int cmp_gpu_available(void)

@@ -53,6 +53,8 @@ struct DecArgs {
 	uint32_t msub; // subsequences per frame allocated in the arrays below
 	uint32_t *exit_a, *exit_b, *cnt, *base, *changed;
 	uint16_t *tile_sum;
+	const uint16_t *model; // MODEL frames: frame f's model at model + f * model_stride bytes
+	uint64_t model_stride;
 };
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t v)
@@ -188,7 +190,7 @@ __global__ void dec_hdr_kernel(DecArgs a)
 	if (a.src_cap < 16u || !(b[0] >> 7) || version != 600u || csize > a.src_cap || csize < hs + (ck ? 4u : 0u) ||
 	    (osize & 1u))
 		st = ERRV(E_INT_HDR);
-	else if (I.pre > 1u) // MODEL / IWT frames are not decoded here
+	else if (I.pre == 2u || (I.pre == 3u && !a.model)) // IWT; MODEL without its model
 		st = ERRV(E_PARAMS_INVALID);
 	else if (I.enc > 2u)
 		st = ERRV(E_INT_ENCODER);
@@ -486,6 +488,20 @@ __global__ __launch_bounds__(256) void dec_tile_scan_kernel(DecArgs a, uint32_t 
 	}
 }
 
+// MODEL (preprocess.c:406-411) inverse: x[i] = r[i] + model[i] (int16 wrap)
+__global__ __launch_bounds__(256) void dec_model_kernel(DecArgs a)
+{
+	const uint32_t f = blockIdx.y, t = blockIdx.x * 256u + threadIdx.x;
+	const DecInfo I = a.info[f];
+	if (I.status || I.pre != 3u)
+		return;
+	uint16_t *x = a.dst + (uint64_t)f * (a.dst_stride / 2u);
+	const uint16_t *m = reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint8_t *>(a.model) +
+							       (uint64_t)f * a.model_stride);
+	for (uint32_t i = t; i < I.n; i += gridDim.x * 256u)
+		x[i] = (uint16_t)(x[i] + m[i]);
+}
+
 __global__ void dec_status_kernel(DecArgs a)
 {
 	const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
@@ -510,7 +526,7 @@ using namespace airsdec;
 // parse and to test for a settled parse.
 extern "C" uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
 				   uint32_t src_cap, uint32_t num_frames, uint16_t *dst, uint64_t dst_stride,
-				   uint32_t dst_samples, uint32_t *status)
+				   uint32_t dst_samples, uint32_t *status, const uint16_t *model, uint64_t model_stride)
 {
 	if (!e || !src || !dst || !status || !num_frames || (src_stride & 7u) || ((uintptr_t)src & 7u) ||
 	    ((uintptr_t)dst & 1u) || (dst_stride & 1u))
@@ -526,6 +542,8 @@ extern "C" uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, 
 	a.dst_stride = dst_stride;
 	a.dst_samples = dst_samples;
 	a.status = status;
+	a.model = model;
+	a.model_stride = model_stride;
 	// frame info + the largest subsequence count
 	uint8_t *hdr = (uint8_t *)airs_dev_scratch(e, AIRS_NSLOT - 2, (size_t)num_frames * sizeof(DecInfo) + 64u);
 	if (!hdr)
@@ -579,6 +597,9 @@ extern "C" uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, 
 		hipLaunchKernelGGL(dec_tile_sum_kernel, tg, dim3(256), 0, s, a, tiles);
 		hipLaunchKernelGGL(dec_tile_prefix_kernel, dim3(num_frames), dim3(1024), 0, s, a, tiles);
 		hipLaunchKernelGGL(dec_tile_scan_kernel, tg, dim3(256), 0, s, a, tiles);
+		if (model)
+			hipLaunchKernelGGL(dec_model_kernel, dim3(min((max_n + 255u) / 256u, 256u), num_frames), dim3(256), 0,
+					   s, a);
 	}
 	hipLaunchKernelGGL(dec_status_kernel, dim3((num_frames + 255u) / 256u), dim3(256), 0, s, a);
 	DCHECK(hipGetLastError());

@@ -81,9 +81,10 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *engine, struct cmp_context *ctx
 /* Decoder (no reference counterpart: the reference has none, see
  * programs/airspacecli.c:421-423).  Decodes num_frames frames as written by
  * cmp_compress_* / cmp_gpu_compress back into their 16-bit samples (the low
- * halves, for i16-in-i32 sources).  Frames with NONE or DIFF preprocessing and
- * any encoder; MODEL and IWT frames get CMP_ERR_PARAMS_INVALID.  The checksum
- * is not verified. */
+ * halves, for i16-in-i32 sources).  Frames with NONE, DIFF or (given the model
+ * each frame was encoded against) MODEL preprocessing and any encoder; IWT
+ * frames, and MODEL frames without a model, get CMP_ERR_PARAMS_INVALID.  The
+ * checksum is not verified. */
 struct cmp_gpu_decode_batch {
 	const void *src;        /* device; frame i at src + i*src_stride, 8-byte aligned */
 	uint64_t src_stride;    /* bytes, multiple of 8, >= src_capacity */
@@ -93,6 +94,8 @@ struct cmp_gpu_decode_batch {
 	uint64_t dst_stride;    /* bytes, even */
 	uint32_t dst_samples;   /* samples available per frame */
 	uint32_t *status;       /* device [num_frames]: samples decoded, or an error value */
+	const uint16_t *model;  /* device or NULL; frame i's model at model + i*model_stride bytes */
+	uint64_t model_stride;  /* bytes, even */
 };
 
 /* Returns CMP_ERR_NO_ERROR or a call-level error; per-frame results land in

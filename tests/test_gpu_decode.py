@@ -125,3 +125,45 @@ def test_decode_rejects(eng, orc):
     assert api.error_name(status[1]) == "INT_HDR"
     assert api.error_name(status[2]) == "INT_BITSTREAM"
     assert api.error_name(status[3]) == "PARAMS_INVALID"
+
+
+def test_decode_model_frames(eng, orc):
+    """MODEL frames decode against the model each was encoded with: the work
+    buffer as the oracle held it before the call (preprocess.c:406-411)."""
+    import torch
+    rng = np.random.default_rng(5)
+    frames, models, xs = [], [], []
+    for trial in range(6):
+        n = int(rng.choice([1, 17, 4096, 9001]))
+        p = api.CmpParams(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16,
+                          secondary_iterations=3, secondary_preprocessing=3,
+                          secondary_encoder_type=int(rng.choice([0, 1, 2])), secondary_encoder_param=8,
+                          secondary_encoder_outlier=107, model_rate=int(rng.choice([0, 11, 16])))
+        ctx = api.CmpContext()
+        wbs = orc.cal_work_buf_size(p, 2 * n)
+        wb = api.aligned_empty(wbs, fill=0)
+        assert not api.is_error(orc.initialise(ctx, p, wb, wbs))
+        base = np.cumsum(rng.integers(-300, 300, n))
+        for step in range(4):
+            x = ((base + rng.integers(-40, 40, n)) & 0xFFFF).astype(np.uint16)
+            before = np.frombuffer(bytes(wb[:2 * n]), dtype=np.uint16).copy()
+            cap = 26 + 6 * n + 64
+            dst = api.aligned_empty(cap)
+            r = orc.compress_u16(ctx, dst, cap, x)
+            assert not api.is_error(r), api.error_name(r)
+            if step:  # secondary (MODEL) passes
+                frames.append(bytes(dst[:r]))
+                models.append(before)
+                xs.append(x)
+    nmax = max(len(x) for x in xs)
+    mod = np.zeros((len(frames), nmax), dtype=np.uint16)
+    for i, m in enumerate(models):
+        mod[i, :len(m)] = m
+    dmod = torch.from_numpy(mod.view(np.int16)).cuda()
+    import types
+    eng2 = types.SimpleNamespace(decompress=lambda *a: eng.decompress(*a, dmod.data_ptr(), 2 * nmax),
+                                 synchronize=eng.synchronize)
+    status, outs = gpu_decode(eng2, frames, nmax)
+    for i, x in enumerate(xs):
+        assert status[i] == len(x), (i, api.error_name(status[i]) if api.is_error(status[i]) else status[i])
+        assert np.array_equal(outs[i][:len(x)], x), i
