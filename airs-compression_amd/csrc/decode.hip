@@ -190,7 +190,7 @@ __global__ void dec_hdr_kernel(DecArgs a)
 	if (a.src_cap < 16u || !(b[0] >> 7) || version != 600u || csize > a.src_cap || csize < hs + (ck ? 4u : 0u) ||
 	    (osize & 1u))
 		st = ERRV(E_INT_HDR);
-	else if (I.pre == 2u || (I.pre == 3u && !a.model)) // IWT; MODEL without its model
+	else if (I.pre == 3u && !a.model) // MODEL without its model
 		st = ERRV(E_PARAMS_INVALID);
 	else if (I.enc > 2u)
 		st = ERRV(E_INT_ENCODER);
@@ -221,6 +221,8 @@ __global__ void dec_hdr_kernel(DecArgs a)
 		I.nsub = 0;
 	a.info[f] = I;
 	atomicMax(a.maxsub, I.nsub);
+	if (!st && I.pre == 2u)
+		atomicOr(a.maxsub + 2, 1u); // some frame needs the inverse IWT
 }
 
 // one parse round; first = the speculative round (starts at s * DEC_B)
@@ -488,6 +490,82 @@ __global__ __launch_bounds__(256) void dec_tile_scan_kernel(DecArgs a, uint32_t 
 	}
 }
 
+// IWT inverse (preprocess.c:140-221 run backwards): the levels from the
+// largest stride down; in each, the even coefficients are undone first (from
+// their odd neighbours, which the forward even step read), then the odd ones
+// (from the restored even neighbours).  Same int32 intermediates and int16
+// wrap as the forward transform, so it is exact.
+template <typename P>
+__device__ __forceinline__ void iiwt_evens(P y, uint32_t n, uint32_t s, uint32_t t0, uint32_t dt)
+{
+	for (uint32_t t = t0;; t += dt) {
+		const uint64_t i = 2ull * s * t;
+		if (i >= n)
+			break;
+		const int32_t c = y[i];
+		if (i == 0)
+			y[0] = (int16_t)(c - (int16_t)((int32_t)y[s] >> 1));
+		else if (i + s < n)
+			y[i] = (int16_t)(c - (int16_t)(((int32_t)y[i - s] + (int32_t)y[i + s]) >> 2));
+		else
+			y[i] = (int16_t)(c - (int16_t)((int32_t)y[i - s] >> 1));
+	}
+}
+
+template <typename P>
+__device__ __forceinline__ void iiwt_odds(P y, uint32_t n, uint32_t s, uint32_t t0, uint32_t dt)
+{
+	for (uint32_t t = t0;; t += dt) {
+		const uint64_t i = (uint64_t)s + 2ull * s * t;
+		if (i >= n)
+			break;
+		const int32_t c = y[i];
+		y[i] = i + s < n ? (int16_t)(c + (int16_t)(((int32_t)y[i - s] + (int32_t)y[i + s]) >> 1))
+				 : (int16_t)(c + (int32_t)y[i - s]);
+	}
+}
+
+#define DEC_IWT_LDS_MAX 65536u
+// frames up to 64 Ki samples: the whole frame in LDS, one workgroup each
+__global__ __launch_bounds__(1024) void dec_iiwt_frame_kernel(DecArgs a)
+{
+	extern __shared__ int16_t L_f[];
+	const uint32_t f = blockIdx.x, t = threadIdx.x;
+	const DecInfo I = a.info[f];
+	if (I.status || I.pre != 2u || I.n > DEC_IWT_LDS_MAX || I.n < 2u)
+		return;
+	int16_t *x = reinterpret_cast<int16_t *>(a.dst + (uint64_t)f * (a.dst_stride / 2u));
+	for (uint32_t i = t; i < I.n; i += 1024u)
+		L_f[i] = x[i];
+	__syncthreads();
+	uint32_t top = 1;
+	while (2u * top < I.n)
+		top <<= 1;
+	for (uint32_t s = top; s; s >>= 1) {
+		iiwt_evens(L_f, I.n, s, t, 1024u);
+		__syncthreads();
+		iiwt_odds(L_f, I.n, s, t, 1024u);
+		__syncthreads();
+	}
+	for (uint32_t i = t; i < I.n; i += 1024u)
+		x[i] = L_f[i];
+}
+
+// larger frames: one launch per phase per level, in place in dst
+__global__ __launch_bounds__(256) void dec_iiwt_level_kernel(DecArgs a, uint32_t s, uint32_t odds)
+{
+	const uint32_t f = blockIdx.y;
+	const DecInfo I = a.info[f];
+	if (I.status || I.pre != 2u || I.n <= DEC_IWT_LDS_MAX || s >= I.n)
+		return;
+	int16_t *x = reinterpret_cast<int16_t *>(a.dst + (uint64_t)f * (a.dst_stride / 2u));
+	const uint32_t t0 = blockIdx.x * 256u + threadIdx.x, dt = gridDim.x * 256u;
+	if (odds)
+		iiwt_odds(x, I.n, s, t0, dt);
+	else
+		iiwt_evens(x, I.n, s, t0, dt);
+}
+
 // MODEL (preprocess.c:406-411) inverse: x[i] = r[i] + model[i] (int16 wrap)
 __global__ __launch_bounds__(256) void dec_model_kernel(DecArgs a)
 {
@@ -551,11 +629,13 @@ extern "C" uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, 
 	a.info = (DecInfo *)hdr;
 	a.maxsub = (uint32_t *)(hdr + (size_t)num_frames * sizeof(DecInfo));
 	a.changed = a.maxsub + 1;
-	DCHECK(hipMemsetAsync(a.maxsub, 0, 8, s));
+	DCHECK(hipMemsetAsync(a.maxsub, 0, 12, s));
 	hipLaunchKernelGGL(dec_hdr_kernel, dim3((num_frames + 255u) / 256u), dim3(256), 0, s, a);
-	uint32_t msub = 0;
-	DCHECK(hipMemcpyAsync(&msub, a.maxsub, 4, hipMemcpyDeviceToHost, s));
+	uint32_t hv[3] = {0, 0, 0}; // largest subsequence count, (changed), any IWT frame
+	DCHECK(hipMemcpyAsync(hv, a.maxsub, 12, hipMemcpyDeviceToHost, s));
 	DCHECK(hipStreamSynchronize(s));
+	const uint32_t msub = hv[0];
+	const bool any_iwt = hv[2] != 0u;
 	a.msub = msub ? msub : 1u;
 	const uint32_t max_n = dst_samples;
 	const uint32_t tiles = (max_n + DEC_TILE - 1u) / DEC_TILE;
@@ -600,6 +680,27 @@ extern "C" uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, 
 		if (model)
 			hipLaunchKernelGGL(dec_model_kernel, dim3(min((max_n + 255u) / 256u, 256u), num_frames), dim3(256), 0,
 					   s, a);
+		// IWT frames
+		static bool attr = false;
+		if (!attr) {
+			DCHECK(hipFuncSetAttribute((const void *)dec_iiwt_frame_kernel,
+						   hipFuncAttributeMaxDynamicSharedMemorySize, (int)(DEC_IWT_LDS_MAX * 2u)));
+			attr = true;
+		}
+		if (any_iwt)
+			hipLaunchKernelGGL(dec_iiwt_frame_kernel, dim3(num_frames), dim3(1024),
+					   (size_t)min(max_n, DEC_IWT_LDS_MAX) * 2u, s, a);
+		if (any_iwt && max_n > DEC_IWT_LDS_MAX) {
+			uint32_t top = 1;
+			while (2u * top < max_n)
+				top <<= 1;
+			for (uint32_t st = top; st; st >>= 1) {
+				const uint32_t items = (uint32_t)(((uint64_t)max_n + 2ull * st - 1ull) / (2ull * st));
+				const dim3 lg(min((items + 255u) / 256u, 1024u), num_frames);
+				hipLaunchKernelGGL(dec_iiwt_level_kernel, lg, dim3(256), 0, s, a, st, 0u);
+				hipLaunchKernelGGL(dec_iiwt_level_kernel, lg, dim3(256), 0, s, a, st, 1u);
+			}
+		}
 	}
 	hipLaunchKernelGGL(dec_status_kernel, dim3((num_frames + 255u) / 256u), dim3(256), 0, s, a);
 	DCHECK(hipGetLastError());

@@ -81,10 +81,9 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *engine, struct cmp_context *ctx
 /* Decoder (no reference counterpart: the reference has none, see
  * programs/airspacecli.c:421-423).  Decodes num_frames frames as written by
  * cmp_compress_* / cmp_gpu_compress back into their 16-bit samples (the low
- * halves, for i16-in-i32 sources).  Frames with NONE, DIFF or (given the model
- * each frame was encoded against) MODEL preprocessing and any encoder; IWT
- * frames, and MODEL frames without a model, get CMP_ERR_PARAMS_INVALID.  The
- * checksum is not verified. */
+ * halves, for i16-in-i32 sources).  Frames of every preprocessing mode and
+ * encoder; MODEL frames need the model each was encoded against (MODEL frames
+ * without one get CMP_ERR_PARAMS_INVALID).  The checksum is not verified. */
 struct cmp_gpu_decode_batch {
 	const void *src;        /* device; frame i at src + i*src_stride, 8-byte aligned */
 	uint64_t src_stride;    /* bytes, multiple of 8, >= src_capacity */

@@ -167,3 +167,30 @@ def test_decode_model_frames(eng, orc):
     for i, x in enumerate(xs):
         assert status[i] == len(x), (i, api.error_name(status[i]) if api.is_error(status[i]) else status[i])
         assert np.array_equal(outs[i][:len(x)], x), i
+
+
+def test_decode_iwt_frames(eng, orc):
+    """IWT frames: the inverse transform (levels from the largest stride down)
+    restores the samples exactly; whole-frame LDS kernel up to 64 Ki samples,
+    per-level launches above."""
+    rng = np.random.default_rng(9)
+    frames, xs = [], []
+    for n in (1, 2, 3, 5, 7, 8, 100, 4097, 65536, 65537, 200001):
+        for enc, g in ((1, 16), (2, 10), (0, 1)):
+            p = api.CmpParams(primary_preprocessing=2, primary_encoder_type=enc, primary_encoder_param=g,
+                              primary_encoder_outlier=200)
+            ctx = api.CmpContext()
+            wbs = orc.cal_work_buf_size(p, 2 * n)
+            wb = api.aligned_empty(wbs, fill=0)
+            assert not api.is_error(orc.initialise(ctx, p, wb, wbs))
+            x = ((np.cumsum(rng.integers(-500, 500, n)) + rng.integers(-30000, 30000)) & 0xFFFF).astype(np.uint16)
+            cap = 26 + 6 * n + 64
+            dst = api.aligned_empty(cap)
+            r = orc.compress_u16(ctx, dst, cap, x)
+            assert not api.is_error(r), api.error_name(r)
+            frames.append(bytes(dst[:r]))
+            xs.append(x)
+    status, outs = gpu_decode(eng, frames, max(len(x) for x in xs))
+    for i, x in enumerate(xs):
+        assert status[i] == len(x), (i, api.error_name(status[i]) if api.is_error(status[i]) else status[i])
+        assert np.array_equal(outs[i][:len(x)], x), (i, len(x))
