@@ -5,7 +5,7 @@ n=$1; f=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$ROOT/exp/$n"
 cd "$ROOT/airs-compression_amd"
-make -s build/cmp_host.o
+make -s build/cmp_host.o build/decode.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $f -I../include -Icsrc -c csrc/encode.hip -o ../exp/$n/encode.o
-/opt/rocm/bin/hipcc -shared -Wl,-Bsymbolic -Wl,--no-undefined ../exp/$n/encode.o build/cmp_host.o -o ../exp/$n/libairscmp.so
+/opt/rocm/bin/hipcc -shared -Wl,-Bsymbolic -Wl,--no-undefined ../exp/$n/encode.o build/decode.o build/cmp_host.o -o ../exp/$n/libairscmp.so
 rm -f ../exp/$n/encode.o
