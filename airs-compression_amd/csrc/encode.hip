@@ -795,16 +795,30 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 		uint64_t acc = 0u;
 		if (fastk && nv[CH - 1] == EPT) {
 			const char *tab = reinterpret_cast<const char *>(s_rice);
-#pragma unroll
-			for (uint32_t j = 0; j < EPT / 2; j++) {
-				const u16x2 v = __builtin_elementwise_add_sat(pk(mp[CH - 1][j]), (u16x2)(1));
-				const u16x2 qa = __builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17))
-						 << (u16x2)(3);
+			auto pair = [&](uint32_t j) {
+				u16x2 qa;
+				if (AIRS_KEEP_Q) {
+					qa = pk(mq[AIRS_KEEP_Q ? CH - 1 : 0][j]);
+				} else {
+					const u16x2 v = __builtin_elementwise_add_sat(pk(mp[CH - 1][j]), (u16x2)(1));
+					qa = __builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17)) << (u16x2)(3);
+				}
 #pragma unroll
 				for (uint32_t h = 0; h < 2; h++) {
 					const uint2 e = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
 					acc = (acc << e.y) | (half16(mp[CH - 1][j], h) + e.x);
 				}
+			};
+			// every sample takes >= k + 1 bits, so for k >= 3 the lane's last
+			// 32 bits lie in its last 8 samples: the first pairs are skipped
+			if (EPT >= 16 && cd.k >= 3u) {
+#pragma unroll
+				for (uint32_t j = EPT / 4; j < EPT / 2; j++)
+					pair(j);
+			} else {
+#pragma unroll
+				for (uint32_t j = 0; j < EPT / 2; j++)
+					pair(j);
 			}
 		} else {
 #pragma unroll
