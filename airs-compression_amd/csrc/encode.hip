@@ -751,7 +751,7 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 
 	// ---- the segment's last 32 bits (wave 3 rebuilds its last chunk) ------
 #ifndef AIRS_LB_WIN
-#define AIRS_LB_WIN 2
+#define AIRS_LB_WIN 1
 #endif
 	constexpr int LB_WIN = AIRS_LB_WIN; // look-back windows of 64 granules fetched per round
 	uint64_t gv[LB_WIN];
@@ -911,6 +911,15 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 	};
 
 	// ---- phase 2: chunk by chunk: codewords -> LDS image -> HBM -----------
+	// Waves past phase 1 issue ahead of waves of newer segments on the same
+	// SIMD (still in phase 1): the older segment holds LDS and its frame's
+	// look-back chain, so finishing it first shortens residency (measured:
+	// 1-3 % on cfg2 and the cfg4 shard).
+#ifndef AIRS_PRIO_P2
+#define AIRS_PRIO_P2 1
+#endif
+	if (AIRS_PRIO_P2)
+		__builtin_amdgcn_s_setprio(AIRS_PRIO_P2);
 	// rolled loop (keeps register pressure flat): the current chunk's state is
 	// always index 0 of mp/nmp/nv/excl/tot/base/firstc, rotated at the end
 	uint32_t tot_m3 = 0u; // totals of chunks c-3, c-2 (an image is recycled now), c-1
@@ -1032,6 +1041,9 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 		if (c == LBC) {
 			// ---- decoupled look-back (wave 0), overlapped with the packing ----
 			if (wid == 0) {
+#ifdef AIRS_PRIO_LB // experiment: issue priority of the look-back wave
+				__builtin_amdgcn_s_setprio(AIRS_PRIO_LB);
+#endif
 				dbg_stamp(a, gseg, 3);
 				uint32_t Pw = HDR_BITS;
 				if (DBG(2u)) {
@@ -1129,6 +1141,9 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 					s_misc[2] = pred;
 				}
 				dbg_stamp(a, gseg, 2);
+#ifdef AIRS_PRIO_LB
+				__builtin_amdgcn_s_setprio(AIRS_PRIO_P2);
+#endif
 			}
 			__syncthreads();
 			P = __builtin_amdgcn_readfirstlane(s_misc[1]);
