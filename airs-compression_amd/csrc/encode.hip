@@ -926,6 +926,7 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 	uint32_t tot_m2 = 0u;
 	uint32_t tot_m1 = 0u;
 	uint32_t pred_1 = 0u; // (tid 0) last 32 bits of chunk 0, kept for chunk 1's late store
+	uint32_t pred_2 = 0u; // (tid 0) last 32 bits of chunk 1 (four images: chunk 2 is stored late too)
 #ifndef AIRS_CHUNK_UNROLL
 #define AIRS_CHUNK_UNROLL 4
 #endif
@@ -1154,6 +1155,11 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 				store_chunk(L_dyn + 4u, 0u, tot_first, seg_pred, is_last && last_ne == 0u);
 			if (LBC == 2) // so did chunk 1
 				store_chunk(L_dyn + IMGW + 4u, tot_first, tot_m1, pred_1, is_last && last_ne == 1u);
+			if (LBC == 3) { // and, with four images, chunks 1 and 2
+				store_chunk(L_dyn + IMGW + 4u, tot_first, tot_m2, pred_1, is_last && last_ne == 1u);
+				store_chunk(L_dyn + 2u * IMGW + 4u, tot_first + tot_m2, tot_m1, pred_2,
+					    is_last && last_ne == 2u);
+			}
 		}
 
 		if (c >= LBC)
@@ -1189,6 +1195,8 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 		}
 		if (c == 0)
 			pred_1 = pred_next;
+		if (c == 1)
+			pred_2 = pred_next;
 		pred_c = pred_next;
 		// rotate the per-chunk state
 		tot_m3 = tot_m2;
