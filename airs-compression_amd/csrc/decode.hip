@@ -7,16 +7,22 @@
 // orc_decode (oracle/cmp_oracle.c).
 //
 // A Golomb stream has no index, so the payload of each frame is cut into
-// subsequences of DEC_B bits and parsed in parallel by self-synchronisation:
-//   parse 0   thread s decodes codewords from bit s*DEC_B (a guess) until it
-//             passes (s+1)*DEC_B and records where it stopped (its exit)
-//   parse j   thread s decodes from the exit of thread s-1 of parse j-1;
-//             repeated until no exit changes (a wrong guess usually falls
-//             into step with the true parse after a few codewords, so one or
-//             two rounds settle most frames)
-//   scan      per frame, exclusive sum of the symbol counts -> output index
-//   output    each thread decodes its settled range again and writes the
-//             residuals; DIFF frames then take an inclusive int16 prefix sum.
+// subsequences of DEC_B bits and parsed in parallel by self-synchronisation.
+// A workgroup owns DEC_WG consecutive subsequences, a DEC_WG * DEC_B bit
+// span of the stream, which it stages in LDS with coalesced loads:
+//   parse     thread s decodes codewords from a start (a guess: bit s*DEC_B)
+//             until it passes (s+1)*DEC_B and records where it stopped (its
+//             exit); inside the workgroup the starts are then settled in LDS
+//             (thread s restarts from thread s-1's exit until none moves: a
+//             wrong guess usually falls into step with the true parse after a
+//             few codewords, so only the first threads redo any work)
+//   rounds    the workgroup's first start is the previous workgroup's last
+//             exit of the round before; rounds repeat until no workgroup's
+//             last exit moves (workgroups whose first start is unchanged are
+//             skipped)
+//   scan      per frame, exclusive sum of the workgroups' symbol counts
+//   output    each workgroup decodes its settled ranges again and writes the
+//             residuals; DIFF / MODEL / IWT frames are inverted afterwards.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -25,7 +31,12 @@
 
 namespace airsdec {
 
-#define DEC_B 2048u           // bits per subsequence
+#define DEC_B 512u            // bits per subsequence
+#define DEC_WG 256u           // subsequences (threads) per workgroup
+#define DEC_SPANW (DEC_WG * DEC_B / 32u) // stream words a workgroup owns
+#define DEC_HALO 8u           // words past the span (the last codeword and its window)
+#define DEC_PRE 8u            // words before the span (the warm-up of the first range)
+#define DEC_WARM 128u         // bits decoded before a guessed start (speculative round)
 #define DEC_BAD 0xFFFFFFFFu   // exit of a parse that met an invalid codeword
 #define E_GENERIC 1u
 #define E_PARAMS_INVALID 10u
@@ -51,7 +62,9 @@ struct DecArgs {
 	DecInfo *info;
 	uint32_t *maxsub;
 	uint32_t msub; // subsequences per frame allocated in the arrays below
+	uint32_t mwg;  // workgroups per frame allocated in wg_cnt / wg_base
 	uint32_t *exit_a, *exit_b, *cnt, *base, *changed;
+	uint32_t *wg_cnt, *wg_base;
 	uint16_t *tile_sum;
 	const uint16_t *model; // MODEL frames: frame f's model at model + f * model_stride bytes
 	uint64_t model_stride;
@@ -67,21 +80,28 @@ __device__ __forceinline__ uint32_t ilog2(uint32_t x)
 	return 31u - __builtin_clz(x);
 }
 
-// 64 stream bits from absolute frame bit position abit (MSB first); words
-// past the frame's last are clamped to it (their bits are never used)
-__device__ __forceinline__ uint64_t win64(const uint32_t *f32, uint32_t wmax, uint32_t abit)
-{
-	const uint32_t w = abit >> 5, o = abit & 31u;
-	const uint32_t d0 = bswap32(f32[min(w, wmax)]), d1 = bswap32(f32[min(w + 1u, wmax)]),
-		       d2 = bswap32(f32[min(w + 2u, wmax)]);
-	const uint64_t hi = ((uint64_t)d0 << 32) | d1;
-	return o ? (hi << o) | (d2 >> (32u - o)) : hi;
-}
-
 // one codeword at the top of the 64-bit window W: returns its length (0 =
 // invalid) and m, the mapped value (UNCOMPRESSED: the raw 16 bits)
+// RICE: the frame is GOLOMB_ZERO with g = 2^k (cutoff == g, so no extra
+// bit, and q*g is a shift); chosen per frame, block-uniform
+template <bool RICE>
 __device__ __forceinline__ uint32_t dec_window(const DecInfo &I, uint64_t W, uint32_t &m)
 {
+	if (RICE) {
+		const uint32_t q = (uint32_t)__clzll(~W);
+		if (q > 32u)
+			return 0u;
+		uint32_t len = q + 1u + I.k;
+		const uint32_t x = I.k ? (uint32_t)((W << (q + 1u)) >> (64u - I.k)) : 0u;
+		const uint32_t u = (q << I.k) | x;
+		if (u == 0u) {
+			m = (uint32_t)((W << len) >> 48);
+			len += 16u;
+		} else {
+			m = u - 1u;
+		}
+		return len > 48u ? 0u : len;
+	}
 	if (I.enc == 0u) { // UNCOMPRESSED (encoder.c:331-333)
 		m = (uint32_t)(W >> 48);
 		return 16u;
@@ -122,44 +142,46 @@ __device__ __forceinline__ uint32_t dec_window(const DecInfo &I, uint64_t W, uin
 	return len > 48u ? 0u : len;
 }
 
-__device__ __forceinline__ uint32_t dec_symbol(const DecInfo &I, const uint32_t *f32, uint32_t p, uint32_t &m)
-{
-	return dec_window(I, win64(f32, I.wmax, I.hdr_bits + p), m);
-}
-
-// Sequential bit reader: the next stream bits MSB-aligned in buf (nv valid,
-// zeros below), refilled a dword at a time, so a codeword costs a load only
-// every few symbols.  A codeword that does not fit the valid bits (its
-// decoded length exceeds nv: any bit it used past them was a fill zero) is
-// decoded again from memory.
-struct BitReader {
-	const uint32_t *f32;
-	uint32_t wmax, w, nv, p; // next dword, valid bits, payload bit position
+// Sequential bit reader over a workgroup's LDS copy of the stream (words
+// already byte-swapped, so bit 31 of L[i] is the first): the next stream bits
+// MSB-aligned in buf (nv valid, zeros below), refilled a word at a time.  A
+// codeword that does not fit the valid bits (its decoded length exceeds nv:
+// a bit it used past them was a fill zero) is decoded again from a full
+// window read at its position.
+template <bool RICE>
+struct LdsReader {
+	const uint32_t *L;
+	uint32_t w0, w, nv, p; // L[0] holds stream word w0; next word; valid bits; payload bit position
 	uint64_t buf;
-	__device__ __forceinline__ void init(const DecInfo &I, const uint32_t *f, uint32_t pos)
+	__device__ __forceinline__ uint64_t window(const DecInfo &I, uint32_t pos) const
 	{
-		f32 = f;
-		wmax = I.wmax;
+		const uint32_t abit = I.hdr_bits + pos, wi = (abit >> 5) - w0, o = abit & 31u;
+		const uint64_t hi = ((uint64_t)L[wi] << 32) | L[wi + 1u];
+		return o ? (hi << o) | (L[wi + 2u] >> (32u - o)) : hi;
+	}
+	__device__ __forceinline__ void init(const DecInfo &I, const uint32_t *l, uint32_t base_word, uint32_t pos)
+	{
+		L = l;
+		w0 = base_word;
 		p = pos;
-		const uint32_t abit = I.hdr_bits + pos, w0 = abit >> 5, o = abit & 31u;
-		const uint64_t hi = ((uint64_t)bswap32(f32[min(w0, wmax)]) << 32) | bswap32(f32[min(w0 + 1u, wmax)]);
-		buf = hi << o;
+		const uint32_t abit = I.hdr_bits + pos, wi = (abit >> 5) - w0, o = abit & 31u;
+		buf = (((uint64_t)L[wi] << 32) | L[wi + 1u]) << o;
 		nv = 64u - o;
-		w = w0 + 2u;
+		w = wi + 2u;
 	}
 	__device__ __forceinline__ uint32_t next(const DecInfo &I, uint32_t &m)
 	{
 		if (nv <= 32u) {
-			buf |= (uint64_t)bswap32(f32[min(w, wmax)]) << (32u - nv);
+			buf |= (uint64_t)L[w] << (32u - nv);
 			w++;
 			nv += 32u;
 		}
-		uint32_t len = dec_window(I, buf, m);
+		uint32_t len = dec_window<RICE>(I, buf, m);
 		if (len > nv || !len) {
-			len = dec_symbol(I, f32, p, m); // slow path: straight from memory
+			len = dec_window<RICE>(I, window(I, p), m); // slow path: the full window
 			if (!len)
 				return 0u;
-			init(I, f32, p + len);
+			init(I, L, w0, p + len);
 			return len;
 		}
 		buf = len < 64u ? buf << len : 0u;
@@ -168,6 +190,21 @@ struct BitReader {
 		return len;
 	}
 };
+
+// Stage workgroup wg's span of frame f's stream (with DEC_PRE words before
+// it and DEC_HALO after) in LDS, byte-swapped; returns the stream word held
+// in L[0].  Words outside the frame are clamped into it (their bits are never
+// used by a valid parse).
+#define DEC_LDSW (DEC_PRE + DEC_SPANW + DEC_HALO)
+__device__ __forceinline__ uint32_t stage_span(const DecArgs &a, const DecInfo &I, uint32_t f, uint32_t wg,
+					       uint32_t *L)
+{
+	const uint32_t *f32 = reinterpret_cast<const uint32_t *>(a.src + (uint64_t)f * a.src_stride);
+	const int32_t w0 = (int32_t)((I.hdr_bits + wg * DEC_WG * DEC_B) >> 5) - (int32_t)DEC_PRE;
+	for (uint32_t i = threadIdx.x; i < DEC_LDSW; i += DEC_WG)
+		L[i] = bswap32(f32[min((uint32_t)max(w0 + (int32_t)i, 0), I.wmax)]);
+	return (uint32_t)w0; // may be "negative": only differences are used
+}
 
 // header of every frame (header.c:24-67) -> DecInfo; NONE / DIFF frames only
 __global__ void dec_hdr_kernel(DecArgs a)
@@ -225,59 +262,154 @@ __global__ void dec_hdr_kernel(DecArgs a)
 		atomicOr(a.maxsub + 2, 1u); // some frame needs the inverse IWT
 }
 
-// one parse round; first = the speculative round (starts at s * DEC_B)
-__global__ __launch_bounds__(256) void dec_parse_kernel(DecArgs a, const uint32_t *exit_in, uint32_t *exit_out,
-							uint32_t first)
+// decode [start, end) of the stream from LDS: exit position and codeword count
+template <bool RICE>
+__device__ __forceinline__ uint32_t parse_range(const DecInfo &I, const uint32_t *L, uint32_t w0, uint32_t start,
+						uint32_t end, uint32_t &cnt)
 {
-	const uint32_t f = blockIdx.y, s = blockIdx.x * 256u + threadIdx.x;
-	const DecInfo I = a.info[f];
-	if (s >= I.nsub)
-		return;
-	const size_t o = (size_t)f * a.msub + s;
-	const uint32_t start = s == 0u ? 0u : first ? s * DEC_B : exit_in[o - 1u];
-	if (!first && a.base[o] == start) {
-		// same start as last round: same result
-		exit_out[o] = exit_in[o];
-		return;
-	}
-	a.base[o] = start; // the start this round used (before the scan reuses the array)
-	uint32_t p = start, c = 0;
-	if (start != DEC_BAD) {
-		const uint32_t *f32 = reinterpret_cast<const uint32_t *>(a.src + (uint64_t)f * a.src_stride);
-		const uint32_t end = min((s + 1u) * DEC_B, I.nbits);
-		BitReader br;
-		br.init(I, f32, start);
+	cnt = 0;
+	if (start == DEC_BAD)
+		return DEC_BAD;
+	uint32_t p = start;
+	if (p < end) {
+		LdsReader<RICE> br;
+		br.init(I, L, w0, start);
 		while (p < end) {
 			uint32_t m;
 			const uint32_t len = br.next(I, m);
-			if (!len) {
-				p = DEC_BAD;
-				break;
-			}
+			if (!len)
+				return DEC_BAD;
 			p += len;
-			c++;
+			cnt++;
 		}
 	}
-	exit_out[o] = p;
-	a.cnt[o] = c;
-	if (!first && p != exit_in[o])
-		*a.changed = 1u;
+	return p;
 }
 
-// per frame: exclusive scan of the symbol counts (one workgroup)
+// Speculative start of range r0 (> 0): decode from DEC_WARM bits before it
+// and take the first codeword boundary at or past r0.  A Golomb parse falls
+// into step with the true one within a few codewords, so this is almost
+// always where the previous range's parse stops, and the settle pass finds
+// nothing to redo.  DEC_BAD if an invalid codeword came first.
+template <bool RICE>
+__device__ __forceinline__ uint32_t warm_start(const DecInfo &I, const uint32_t *L, uint32_t w0, uint32_t r0)
+{
+	uint32_t p = r0 - min(r0, DEC_WARM);
+	LdsReader<RICE> br;
+	br.init(I, L, w0, p);
+	while (p < r0) {
+		uint32_t m;
+		const uint32_t len = br.next(I, m);
+		if (!len)
+			return r0; // garbage before r0: guess r0 itself
+		p += len;
+	}
+	return p;
+}
+
+// One parse round over workgroup-sized spans (grid: workgroups x frames).
+// first: the speculative round (every start a guess).  Later rounds redo a
+// workgroup only when its first start (the previous workgroup's last exit of
+// the round before) moved, and inside it only the threads whose start moved.
+template <bool RICE>
+__device__ __forceinline__ void parse_wg(const DecArgs &a, const DecInfo &I, const uint32_t *exit_in,
+					 uint32_t *exit_out, uint32_t first, uint32_t *L, uint32_t *s_exit, uint32_t *s_sum)
+{
+	const uint32_t f = blockIdx.y, wg = blockIdx.x, t = threadIdx.x, s = wg * DEC_WG + t;
+	const bool live = s < I.nsub;
+	const size_t o = (size_t)f * a.msub + s, o0 = (size_t)f * a.msub + wg * DEC_WG;
+	uint32_t in_start = wg == 0u ? 0u : first ? 0u : exit_in[o0 - 1u];
+	if (!first && a.base[o0] == in_start) { // block-uniform: nothing moved
+		if (live)
+			exit_out[o] = exit_in[o];
+		return;
+	}
+	const uint32_t w0 = stage_span(a, I, f, wg, L);
+	__syncthreads();
+	if (first && wg) // the first range's start is a warm guess as well
+		in_start = warm_start<RICE>(I, L, w0, wg * DEC_WG * DEC_B);
+	const uint32_t end = min((s + 1u) * DEC_B, I.nbits);
+	uint32_t start, ex = 0, c = 0;
+	if (first) {
+		start = t == 0u && wg == 0u ? 0u : live ? warm_start<RICE>(I, L, w0, s * DEC_B) : 0u;
+		if (live)
+			ex = parse_range<RICE>(I, L, w0, start, end, c);
+	} else {
+		// last round's result stands unless the start moves
+		start = t == 0u ? in_start : a.base[o];
+		if (live) {
+			if (t == 0u) {
+				ex = parse_range<RICE>(I, L, w0, start, end, c);
+			} else {
+				ex = exit_in[o];
+				c = a.cnt[o];
+			}
+		}
+	}
+	for (;;) { // settle: thread t starts where thread t-1 stopped
+		s_exit[t] = ex;
+		__syncthreads();
+		const uint32_t ns = t == 0u ? in_start : s_exit[t - 1u];
+		const bool moved = live && ns != start;
+		if (moved) {
+			start = ns;
+			ex = parse_range<RICE>(I, L, w0, start, end, c);
+		}
+		if (!__syncthreads_or(moved))
+			break;
+	}
+	if (live) {
+		if (!first && ex != exit_in[o] && (t + 1u == DEC_WG || s + 1u == I.nsub))
+			*a.changed = 1u; // the next workgroup's first start moved
+		exit_out[o] = ex;
+		a.cnt[o] = c;
+		a.base[o] = start;
+	}
+	// the workgroup's codeword count
+	uint32_t v = live ? c : 0u;
+	for (uint32_t d = 32; d; d >>= 1)
+		v += __shfl_down(v, d, 64);
+	if ((t & 63u) == 0u)
+		s_sum[t >> 6] = v;
+	__syncthreads();
+	if (t == 0u) {
+		uint32_t tot = 0;
+		for (uint32_t w = 0; w < DEC_WG / 64u; w++)
+			tot += s_sum[w];
+		a.wg_cnt[(size_t)f * a.mwg + wg] = tot;
+	}
+}
+
+__global__ __launch_bounds__(DEC_WG) void dec_parse_kernel(DecArgs a, const uint32_t *exit_in, uint32_t *exit_out,
+							   uint32_t first)
+{
+	__shared__ uint32_t L[DEC_LDSW];
+	__shared__ uint32_t s_exit[DEC_WG];
+	__shared__ uint32_t s_sum[DEC_WG / 64u];
+	const DecInfo I = a.info[blockIdx.y];
+	if (blockIdx.x * DEC_WG >= I.nsub) // block-uniform
+		return;
+	if (I.enc == 1u && I.cutoff == I.g)
+		parse_wg<true>(a, I, exit_in, exit_out, first, L, s_exit, s_sum);
+	else
+		parse_wg<false>(a, I, exit_in, exit_out, first, L, s_exit, s_sum);
+}
+
+// per frame: exclusive scan of the workgroups' codeword counts (one workgroup)
 __global__ __launch_bounds__(1024) void dec_scan_kernel(DecArgs a)
 {
 	__shared__ uint32_t s_w[16];
 	__shared__ uint32_t s_carry;
 	const uint32_t f = blockIdx.x, t = threadIdx.x, lane = t & 63u, wid = t >> 6;
 	const DecInfo I = a.info[f];
+	const uint32_t nwg = (I.nsub + DEC_WG - 1u) / DEC_WG;
 	if (t == 0)
 		s_carry = 0;
 	__syncthreads();
-	for (uint32_t b0 = 0; b0 < I.nsub; b0 += 1024u) {
-		const uint32_t s = b0 + t;
-		const size_t o = (size_t)f * a.msub + s;
-		const uint32_t v = s < I.nsub ? a.cnt[o] : 0u;
+	for (uint32_t b0 = 0; b0 < nwg; b0 += 1024u) {
+		const uint32_t i = b0 + t;
+		const size_t o = (size_t)f * a.mwg + i;
+		const uint32_t v = i < nwg ? a.wg_cnt[o] : 0u;
 		uint32_t inc = v;
 		for (uint32_t d = 1; d < 64u; d <<= 1) {
 			const uint32_t y = __shfl_up(inc, d, 64);
@@ -290,8 +422,8 @@ __global__ __launch_bounds__(1024) void dec_scan_kernel(DecArgs a)
 		uint32_t woff = s_carry;
 		for (uint32_t w = 0; w < wid; w++)
 			woff += s_w[w];
-		if (s < I.nsub)
-			a.base[o] = woff + inc - v;
+		if (i < nwg)
+			a.wg_base[o] = woff + inc - v;
 		__syncthreads();
 		if (t == 1023u)
 			s_carry = woff + inc;
@@ -306,26 +438,42 @@ __global__ __launch_bounds__(1024) void dec_scan_kernel(DecArgs a)
 }
 
 // residuals (ZigZag undone) into dst; DIFF frames are summed afterwards
-__global__ __launch_bounds__(256) void dec_out_kernel(DecArgs a, const uint32_t *exits)
+template <bool RICE>
+__device__ __forceinline__ void out_wg(const DecArgs &a, const DecInfo &I, const uint32_t *exits, uint32_t *L,
+				       uint32_t *s_w)
 {
-	const uint32_t f = blockIdx.y, s = blockIdx.x * 256u + threadIdx.x;
-	const DecInfo I = a.info[f];
-	if (s >= I.nsub || I.status)
-		return;
+	const uint32_t f = blockIdx.y, wg = blockIdx.x, t = threadIdx.x, s = wg * DEC_WG + t, lane = t & 63u,
+		       wid = t >> 6;
+	const bool live = s < I.nsub;
 	const size_t o = (size_t)f * a.msub + s;
-	const uint32_t b0 = a.base[o];
+	const uint32_t w0 = stage_span(a, I, f, wg, L);
+	// this thread's first output index: the workgroup's base + its prefix
+	const uint32_t v = live ? a.cnt[o] : 0u;
+	uint32_t inc = v;
+	for (uint32_t d = 1; d < 64u; d <<= 1) {
+		const uint32_t y = __shfl_up(inc, d, 64);
+		if (lane >= d)
+			inc += y;
+	}
+	if (lane == 63u)
+		s_w[wid] = inc;
+	__syncthreads(); // also: the span is staged
+	uint32_t b0 = a.wg_base[(size_t)f * a.mwg + wg] + inc - v;
+	for (uint32_t w = 0; w < wid; w++)
+		b0 += s_w[w];
+	if (!live)
+		return;
 	uint32_t p = s ? exits[o - 1u] : 0u, j = b0;
 	const uint32_t end = min((s + 1u) * DEC_B, I.nbits);
-	const uint32_t *f32 = reinterpret_cast<const uint32_t *>(a.src + (uint64_t)f * a.src_stride);
 	uint16_t *out = a.dst + (uint64_t)f * (a.dst_stride / 2u);
 	// samples are shifted into a 128-bit register and leave as 16-byte stores
 	// of 8 (their run is contiguous; each lane's run starts anywhere), with
 	// 2-byte stores for the unaligned ends
 	const bool vec = (((uintptr_t)out | a.dst_stride) & 15u) == 0;
 	uint64_t lo = 0, hi = 0;
-	BitReader br;
+	LdsReader<RICE> br;
 	if (p < end)
-		br.init(I, f32, p);
+		br.init(I, L, w0, p);
 	while (p < end && j < I.n) {
 		uint32_t m;
 		const uint32_t len = br.next(I, m);
@@ -358,6 +506,19 @@ __global__ __launch_bounds__(256) void dec_out_kernel(DecArgs a, const uint32_t 
 			out[i] = (uint16_t)(sh >= 64u ? hi >> (sh - 64u) : lo >> sh);
 		}
 	}
+}
+
+__global__ __launch_bounds__(DEC_WG) void dec_out_kernel(DecArgs a, const uint32_t *exits)
+{
+	__shared__ uint32_t L[DEC_LDSW];
+	__shared__ uint32_t s_w[DEC_WG / 64u];
+	const DecInfo I = a.info[blockIdx.y];
+	if (blockIdx.x * DEC_WG >= I.nsub || I.status) // block-uniform
+		return;
+	if (I.enc == 1u && I.cutoff == I.g)
+		out_wg<true>(a, I, exits, L, s_w);
+	else
+		out_wg<false>(a, I, exits, L, s_w);
 }
 
 // DIFF (preprocess.c:284-290) inverse: x[i] = x[i-1] + r[i] (int16 wrap), a
@@ -639,8 +800,9 @@ extern "C" uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, 
 	a.msub = msub ? msub : 1u;
 	const uint32_t max_n = dst_samples;
 	const uint32_t tiles = (max_n + DEC_TILE - 1u) / DEC_TILE;
-	const size_t per = (size_t)num_frames * a.msub * 4u;
-	const size_t need = 4u * per + (size_t)num_frames * tiles * 2u + 64u;
+	a.mwg = (a.msub + DEC_WG - 1u) / DEC_WG;
+	const size_t per = (size_t)num_frames * a.msub * 4u, per_wg = (size_t)num_frames * a.mwg * 4u;
+	const size_t need = 4u * per + 2u * per_wg + (size_t)num_frames * tiles * 2u + 64u;
 	// the decoder's own slot (the device layer keeps AIRS_NSLOT-1 for IWT)
 	uint8_t *big = (uint8_t *)airs_dev_scratch(e, AIRS_NSLOT - 3, need);
 	if (!big)
@@ -649,30 +811,31 @@ extern "C" uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, 
 	a.exit_b = (uint32_t *)(big + per);
 	a.cnt = (uint32_t *)(big + 2u * per);
 	a.base = (uint32_t *)(big + 3u * per);
-	a.tile_sum = (uint16_t *)(big + 4u * per);
+	a.wg_cnt = (uint32_t *)(big + 4u * per);
+	a.wg_base = (uint32_t *)(big + 4u * per + per_wg);
+	a.tile_sum = (uint16_t *)(big + 4u * per + 2u * per_wg);
 	if (msub) {
-		const dim3 grid((a.msub + 255u) / 256u, num_frames);
+		const dim3 grid(a.mwg, num_frames);
 		if (num_frames > 65535u)
 			return ERRV(E_GENERIC);
 		uint32_t *ein = a.exit_a, *eout = a.exit_b;
-		hipLaunchKernelGGL(dec_parse_kernel, grid, dim3(256), 0, s, a, (const uint32_t *)nullptr, ein, 1u);
-		// rounds until no exit moves (two before the first test)
-		for (uint32_t round = 1; round <= a.msub + 1u; round++) {
+		hipLaunchKernelGGL(dec_parse_kernel, grid, dim3(DEC_WG), 0, s, a, (const uint32_t *)nullptr, ein, 1u);
+		// rounds until no workgroup's last exit moves (each round passes the
+		// corrections one workgroup on, so mwg + 1 rounds always settle)
+		for (uint32_t round = 1; round <= a.mwg + 1u; round++) {
 			DCHECK(hipMemsetAsync(a.changed, 0, 4, s));
-			hipLaunchKernelGGL(dec_parse_kernel, grid, dim3(256), 0, s, a, (const uint32_t *)ein, eout, 0u);
+			hipLaunchKernelGGL(dec_parse_kernel, grid, dim3(DEC_WG), 0, s, a, (const uint32_t *)ein, eout, 0u);
 			uint32_t *tmp = ein;
 			ein = eout;
 			eout = tmp;
-			if (round >= 2u) {
-				uint32_t ch = 1;
-				DCHECK(hipMemcpyAsync(&ch, a.changed, 4, hipMemcpyDeviceToHost, s));
-				DCHECK(hipStreamSynchronize(s));
-				if (!ch)
-					break;
-			}
+			uint32_t ch = 1;
+			DCHECK(hipMemcpyAsync(&ch, a.changed, 4, hipMemcpyDeviceToHost, s));
+			DCHECK(hipStreamSynchronize(s));
+			if (!ch)
+				break;
 		}
 		hipLaunchKernelGGL(dec_scan_kernel, dim3(num_frames), dim3(1024), 0, s, a);
-		hipLaunchKernelGGL(dec_out_kernel, grid, dim3(256), 0, s, a, (const uint32_t *)ein);
+		hipLaunchKernelGGL(dec_out_kernel, grid, dim3(DEC_WG), 0, s, a, (const uint32_t *)ein);
 		const dim3 tg(tiles, num_frames);
 		hipLaunchKernelGGL(dec_tile_sum_kernel, tg, dim3(256), 0, s, a, tiles);
 		hipLaunchKernelGGL(dec_tile_prefix_kernel, dim3(num_frames), dim3(1024), 0, s, a, tiles);
