@@ -144,10 +144,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # AIRS_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on
+    # fewer GPUs (use with --no-gather); the measured runs use RCCL ("nccl")
+    backend = os.environ.get("AIRS_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local % ndev if ndev else local
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
@@ -205,7 +213,7 @@ def main():
     barrier()
     wall = time.perf_counter() - t0
     kern_avg_ms = ev0.elapsed_time(ev1) / args.steps
-    t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    t = torch.tensor([wall], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
