@@ -31,12 +31,16 @@
 
 namespace airsdec {
 
+#ifndef DEC_B
 #define DEC_B 512u            // bits per subsequence
+#endif
 #define DEC_WG 256u           // subsequences (threads) per workgroup
 #define DEC_SPANW (DEC_WG * DEC_B / 32u) // stream words a workgroup owns
 #define DEC_HALO 8u           // words past the span (the last codeword and its window)
 #define DEC_PRE 8u            // words before the span (the warm-up of the first range)
-#define DEC_WARM 128u         // bits decoded before a guessed start (speculative round)
+#ifndef DEC_WARM
+#define DEC_WARM 192u         // bits decoded before a guessed start (speculative round; <= 32 * DEC_PRE)
+#endif
 #define DEC_BAD 0xFFFFFFFFu   // exit of a parse that met an invalid codeword
 #define E_GENERIC 1u
 #define E_PARAMS_INVALID 10u
