@@ -21,8 +21,9 @@
  * Decompression (the reference's default mode prints "Decompression not
  * implemented yet", airspacecli.c:421-423) is an extension here: the frames
  * of each .air input are decoded on the GPU with cmp_gpu_decompress() and
- * written back as big-endian 16-bit samples, MODEL frames against the model
- * rebuilt from the frames before them.
+ * written back as big-endian 16-bit samples: runs of frames other than MODEL
+ * as one batch, each MODEL frame alone, against the model rebuilt from the
+ * frames before it.
  */
 #include <errno.h>
 #include <getopt.h>
@@ -650,29 +651,61 @@ static int decompress_file(struct job *j, struct dev *d, int fi)
 		size_t o = 0;
 
 		for (pos = 0; pos < size;) {
-			const uint32_t fs = be24(raw + pos + 2), n = be24(raw + pos + 5) / 2u;
-			const uint32_t pre = raw[pos + 15] >> 4;
-			/* zero-padded to a multiple of 8 bytes, at least 24 */
-			const uint32_t cap = fs < 24u ? 24u : (fs + 7u) & ~7u;
+			/* a run: one MODEL frame (it needs the frame before it), or
+			 * consecutive other frames, decoded as one batch */
+			const uint32_t pre0 = raw[pos + 15] >> 4;
+			size_t q = pos, nrun = 0, cap = 24, nmax = 1, dstride, i;
 			struct cmp_gpu_decode_batch b;
-			uint32_t e, status;
+			uint8_t *stage;
+			uint16_t *x;
+			uint32_t *st, e;
 
-			/* one frame per call: a MODEL frame needs the frame before it */
-			if (dev_reserve(&d->src, &d->src_cap, cap) || dev_reserve(&d->dst, &d->dst_cap, 2u * (size_t)n + 2u))
+			for (;;) {
+				const uint32_t fs = be24(raw + q + 2), n = be24(raw + q + 5) / 2u;
+				const size_t c = fs < 24u ? 24u : ((size_t)fs + 7u) & ~(size_t)7u;
+				const size_t ncap = c > cap ? c : cap, nn = n > nmax ? n : nmax;
+
+				if (nrun && ((nrun + 1u) * (ncap + 2u * nn + 16u) > BATCH_BYTES || nrun == 65535u))
+					break;
+				cap = ncap;
+				nmax = nn;
+				nrun++;
+				q += fs;
+				if (pre0 == CMP_PREPROCESS_MODEL || q >= size || (raw[q + 15] >> 4) == CMP_PREPROCESS_MODEL)
+					break;
+			}
+			dstride = (2u * nmax + 15u) & ~(size_t)15u; /* 16-byte rows: vector stores */
+			if (dev_reserve(&d->src, &d->src_cap, nrun * cap) ||
+			    dev_reserve(&d->dst, &d->dst_cap, nrun * dstride) ||
+			    dev_reserve(&d->sizes, &d->sizes_cap, 4u * nrun))
 				goto out;
-			if (hipMemset(d->src, 0, cap) != hipSuccess ||
-			    hipMemcpy(d->src, raw + pos, fs, hipMemcpyHostToDevice) != hipSuccess)
+			stage = calloc(nrun, cap);
+			if (!stage) {
+				log_errno("Memory allocation failed");
+				goto out;
+			}
+			for (i = 0, q = pos; i < nrun; i++) {
+				const uint32_t fs = be24(raw + q + 2);
+
+				memcpy(stage + i * cap, raw + q, fs);
+				q += fs;
+			}
+			e = hipMemcpy(d->src, stage, nrun * cap, hipMemcpyHostToDevice) == hipSuccess;
+			free(stage);
+			if (!e)
 				goto gpu_fail;
 			memset(&b, 0, sizeof(b));
 			b.src = d->src;
 			b.src_stride = cap;
-			b.src_capacity = cap;
-			b.num_frames = 1;
+			b.src_capacity = (uint32_t)cap;
+			b.num_frames = (uint32_t)nrun;
 			b.dst = d->dst;
-			b.dst_stride = 2u * (uint64_t)n + 2u;
-			b.dst_samples = n;
+			b.dst_stride = dstride;
+			b.dst_samples = (uint32_t)nmax;
 			b.status = d->sizes;
-			if (pre == CMP_PREPROCESS_MODEL) {
+			if (pre0 == CMP_PREPROCESS_MODEL) {
+				const uint32_t n = be24(raw + pos + 5) / 2u;
+
 				if (model_n != n) {
 					log_msg(LOG_ERROR, "%s: MODEL frame without a preceding frame of its size",
 						display(j->in[fi]));
@@ -692,39 +725,47 @@ static int decompress_file(struct job *j, struct dev *d, int fi)
 				log_cmp(e, "Decompression failed for %s", display(j->in[fi]));
 				goto out;
 			}
-			if (hipMemcpy(&status, d->sizes, 4, hipMemcpyDeviceToHost) != hipSuccess)
+			st = xmalloc(4u * nrun);
+			x = xmalloc(nrun * dstride);
+			if (hipMemcpy(st, d->sizes, 4u * nrun, hipMemcpyDeviceToHost) != hipSuccess ||
+			    hipMemcpy(x, d->dst, nrun * dstride, hipMemcpyDeviceToHost) != hipSuccess) {
+				free(st);
+				free(x);
 				goto gpu_fail;
-			if (cmp_is_error(status) || status != n) {
-				log_cmp(cmp_is_error(status) ? status : (uint32_t)-(int32_t)CMP_ERR_INT_BITSTREAM,
-					"Decompression failed for %s", display(j->in[fi]));
-				goto out;
 			}
-			{
-				uint16_t *x = xmalloc(2u * (size_t)n + 2u);
+			for (i = 0; i < nrun; i++) {
+				const uint32_t n = be24(raw + pos + 5) / 2u;
+				const uint16_t *xi = (const uint16_t *)((const uint8_t *)x + i * dstride);
 				uint32_t k;
 
-				if (hipMemcpy(x, d->dst, 2u * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) {
+				if (cmp_is_error(st[i]) || st[i] != n) {
+					log_cmp(cmp_is_error(st[i]) ? st[i] : (uint32_t) - (int32_t)CMP_ERR_INT_BITSTREAM,
+						"Decompression failed for %s", display(j->in[fi]));
+					free(st);
 					free(x);
-					goto gpu_fail;
+					goto out;
 				}
-				if (model_n != n) {
-					free(model);
-					model = xmalloc(2u * (size_t)n + 2u);
-					model_n = n;
-					if (d_model) {
-						hipFree(d_model);
-						d_model = NULL;
-					}
-				}
-				next_model(model, x, n, pre == CMP_PREPROCESS_MODEL, raw[pos + 16]);
 				for (k = 0; k < n; k++) {
-					out[o + 2u * k] = (uint8_t)(x[k] >> 8);
-					out[o + 2u * k + 1u] = (uint8_t)x[k];
+					out[o + 2u * k] = (uint8_t)(xi[k] >> 8);
+					out[o + 2u * k + 1u] = (uint8_t)xi[k];
 				}
 				o += 2u * (size_t)n;
-				free(x);
+				if (i + 1u == nrun) { /* the model the next frame may need */
+					if (model_n != n) {
+						free(model);
+						model = xmalloc(2u * (size_t)n + 2u);
+						model_n = n;
+						if (d_model) {
+							hipFree(d_model);
+							d_model = NULL;
+						}
+					}
+					next_model(model, xi, n, pre0 == CMP_PREPROCESS_MODEL, raw[pos + 16]);
+				}
+				pos += be24(raw + pos + 2);
 			}
-			pos += fs;
+			free(st);
+			free(x);
 		}
 	}
 	{
