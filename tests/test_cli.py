@@ -240,3 +240,15 @@ def test_to_string_parse_roundtrip(parser):
                         model_rate=11, checksum_enabled=1, uncompressed_fallback_enabled=0)
     st, back = parser[0](parser[1](par), api.CmpParams())
     assert st == OK and raw(back) == raw(par)
+
+
+def test_decompress_rejects_broken_frames(cli, tmp_path):
+    """The frame walk (24-bit sizes in each header) runs before any GPU work."""
+    bad = tmp_path / "bad.air"
+    bad.write_bytes(b"\x80\x01\x00\x00\x40" + b"\0" * 20)  # size 64 > file
+    r = cli([bad])
+    assert r.returncode == 1 and b"not a valid AIRSPACE frame at byte 0" in r.stderr
+    short = tmp_path / "short.air"
+    short.write_bytes(b"\x80\x01\x00\x00\x10" + b"\0" * 11 + b"\x80")  # one whole 16-byte frame + 1 byte
+    r = cli([short])
+    assert r.returncode == 1 and b"at byte 16" in r.stderr
