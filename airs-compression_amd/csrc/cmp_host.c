@@ -8,6 +8,7 @@
  * without a usable GPU the compress calls fail with CMP_ERR_GENERIC and a
  * message on stderr.
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -305,6 +306,12 @@ struct pass {
 
 enum { SLOT_SRC = 0, SLOT_DST, SLOT_MODEL, SLOT_STATUS, SLOT_CK, SLOT_IDS, SLOT_G, SLOT_AUX, SLOT_FL, SLOT_SIZES };
 
+/* The host-pointer API stages every frame through one process-wide engine
+ * (device scratch slots, look-back state).  Calls on different contexts may
+ * come from different threads (the reference allows one context per thread),
+ * so host_compress() holds g_host_lock for the whole call: calls are
+ * serialised, and the engine is created once, under the lock. */
+static pthread_mutex_t g_host_lock = PTHREAD_MUTEX_INITIALIZER;
 static struct airs_dev_engine *g_host_dev;
 
 static struct airs_dev_engine *host_dev(void)
@@ -516,7 +523,7 @@ static uint32_t host_compress(struct cmp_context *ctx, void *dst, uint32_t cap, 
 			      uint32_t size, enum sample_kind kind)
 {
 	struct frame_io io;
-	uint32_t stride = kind == KIND_I16_IN_I32 ? 4u : 2u;
+	uint32_t stride = kind == KIND_I16_IN_I32 ? 4u : 2u, r;
 
 	/* reference sample_reader.h:19-51 */
 	if (!src)
@@ -528,7 +535,10 @@ static uint32_t host_compress(struct cmp_context *ctx, void *dst, uint32_t cap, 
 	io.n = size / stride;
 	io.bytes = stride;
 	io.kind = kind;
-	return host_generic(ctx, dst, cap, &io);
+	pthread_mutex_lock(&g_host_lock);
+	r = host_generic(ctx, dst, cap, &io);
+	pthread_mutex_unlock(&g_host_lock);
+	return r;
 }
 
 uint32_t cmp_compress_u16(struct cmp_context *ctx, void *dst, uint32_t dst_capacity, const uint16_t *src,
@@ -997,6 +1007,19 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		return ERRV(PARAMS_INVALID);
 	n = b->src_size / bytes;
 	total = num_ctx * fpc;
+	/* frames of a batch must not overlap: every workgroup of a frame writes
+	 * up to min(capacity, worst-case frame) bytes from its frame base */
+	if (total > 1) {
+		const uint64_t worst = frame_worst(n), span = b->dst_capacity < worst ? b->dst_capacity : worst;
+
+		if (b->src_stride < b->src_size || b->dst_stride < span) {
+			fprintf(stderr, "airscmp: cmp_gpu_compress: frames overlap (src_stride %llu < src_size %u "
+					"or dst_stride %llu < %llu)\n",
+				(unsigned long long)b->src_stride, b->src_size, (unsigned long long)b->dst_stride,
+				(unsigned long long)span);
+			return ERRV(GENERIC);
+		}
+	}
 	for (c = 0; c < num_ctx; c++) {
 		if (ctx[c].magic != CTX_MAGIC)
 			return ERRV(CONTEXT_INVALID);
@@ -1019,10 +1042,19 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		free(ptrs);
 		return ERRV(GENERIC);
 	}
-	/* a frame that can fail (capacity below the worst case) changes its
-	 * context's next pass: such batches run step by step */
+	/* a frame that can fail changes its context's next pass (the reference
+	 * does not advance sequence_number on an error), so such batches run step
+	 * by step: capacity below the worst case, or a worst case past the 24-bit
+	 * size field (n > ~2.8 Mi samples: HDR_CMP_SIZE_TOO_LARGE is possible)
+	 * when a context has secondary passes.  Without secondary passes every
+	 * frame is a primary pass with one identifier draw whatever the outcome
+	 * of the frame before, so the plan does not depend on it. */
 	if ((uint64_t)b->dst_capacity < HDR_MAX_SIZE + CMP_CHECKSUM_SIZE + payload_bound(2u * n))
 		exact = 1;
+	if (is_err(cmp_compress_bound(2u * n)) && fpc > 1)
+		for (c = 0; c < num_ctx; c++)
+			if (ctx[c].params.secondary_iterations)
+				exact = 1;
 	if (!exact) {
 		/* replay the context state machine in call order (c-major), counting
 		 * identifier draws; a frame the host API would reject sends the

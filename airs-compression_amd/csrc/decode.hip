@@ -231,6 +231,8 @@ __global__ void dec_hdr_kernel(DecArgs a)
 	if (a.src_cap < 16u || !(b[0] >> 7) || version != 600u || csize > a.src_cap || csize < hs + (ck ? 4u : 0u) ||
 	    (osize & 1u))
 		st = ERRV(E_INT_HDR);
+	else if (I.pre > 3u) // no such preprocessing (cmp.h: NONE, DIFF, IWT, MODEL)
+		st = ERRV(E_INT_HDR);
 	else if (I.pre == 3u && !a.model) // MODEL without its model
 		st = ERRV(E_PARAMS_INVALID);
 	else if (I.enc > 2u)

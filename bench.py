@@ -5,14 +5,25 @@ One step = one cmp_gpu_compress() call over this rank's batch of frames whose
 samples are already resident in HBM (BASELINE.json metric: encode GB/s on the
 uncompressed input, 1 GB = 1e9 B, bit-exact vs the CPU reference).
 
-  N = 1 (default)   configs[1]: 64 Mi u16 samples as 16 frames x 4 Mi
-                    (the 24-bit header size field caps a frame at 8 388 607
-                    samples), DIFF + GOLOMB_ZERO g = 32
-  N > 1             configs[3] sharded round-robin: rank r encodes frames
-                    f = r + N*j, j < 1024, of 64 Ki u16 samples (weak scaling:
-                    128 MiB per GPU, so N = 8 is the 8192-frame config); the
-                    compressed frames are then gathered to rank 0 over RCCL
-                    (timed separately, not part of `value`)
+Workloads (BASELINE.json configs):
+
+  cfg2  (default at N = 1) configs[1]: 64 Mi u16 samples as 16 frames x 4 Mi
+        (the 24-bit header size field caps a frame at 8 388 607 samples),
+        DIFF + GOLOMB_ZERO g = 32
+  cfg3  configs[2]: 1024 frames x 64 Ki u16, W_f = 2^(f mod 12), DIFF +
+        GOLOMB_ZERO with the per-frame Rice k (CMP_GPU_AUTO_RICE)
+  cfg4  (default at N > 1) configs[3]: frames of 64 Ki u16 sharded round-robin,
+        1024 per rank (weak scaling: 128 MiB per GPU, N = 8 is the 8192-frame
+        config); the compressed frames are then gathered to rank 0 (timed
+        separately, not part of `value`)
+  cfg5  configs[4]: 256 streams x 16 acquisitions x 64 Ki i16-in-i32 samples;
+        acquisition 0 DIFF + ZERO g = 16, 1-15 MODEL + MULTI g = 8 o = 107
+        rate 11 (one step = all 4096 frames, 16 launches)
+
+Cold inputs: the timed steps rotate over enough input/output buffer sets that
+one rotation touches more than the 256 MiB Infinity Cache, so every step reads
+its samples from HBM (MI355X_MICROARCH.md, Infinity Cache residency rule).  A
+warm replay of one buffer set is reported beside it under "warm".
 
 Prints ONE JSON line on rank 0.  Diagnostics go to stderr.
 """
@@ -21,7 +32,10 @@ import ctypes
 import hashlib
 import importlib.util
 import json
+import math
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -31,6 +45,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(ROOT, "airs-compression_amd")
 METRIC = "encode GB/s (uncompressed in) on 16-bit frames; bit-exact vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+INFINITY_CACHE = 256 << 20
+DIFF, MODEL, ZERO, MULTI = 1, 3, 1, 2
 
 
 def log(*a):
@@ -46,21 +62,53 @@ def load_pkg():
     return mod
 
 
+CFG_ZERO32 = dict(primary_preprocessing=DIFF, primary_encoder_type=ZERO, primary_encoder_param=32)
 WORKLOADS = {
     "cfg2": dict(desc="configs[1]: 64 Mi u16 samples as 16 frames x 4 Mi, DIFF + GOLOMB_ZERO g=32",
-                 n=4 << 20, frames=16, seed=0xA1A6, W=32, golden="cfg2_64Mi", layout="block"),
+                 kind="u16", n=4 << 20, nctx=1, fpc=16, seed=0xA1A6, W=32, golden="cfg2_64Mi",
+                 layout="block", params=CFG_ZERO32),
+    "cfg3": dict(desc="configs[2]: 1024 frames x 64 Ki u16, W_f = 2^(f mod 12), DIFF + GOLOMB_ZERO with "
+                      "the per-frame Rice k (CMP_GPU_AUTO_RICE)",
+                 kind="u16", n=64 << 10, nctx=1, fpc=1024, seed=0xA1A7, W="pow2_mod12", golden="cfg3_autorice",
+                 layout="block", auto_rice=True, params=CFG_ZERO32),
     "cfg4": dict(desc="configs[3]: frames of 64 Ki u16, round-robin over GPUs (1024 per GPU), "
                       "DIFF + GOLOMB_ZERO g=32",
-                 n=64 << 10, frames=1024, seed=0xA1A8, W=32, golden="cfg4_8192", layout="roundrobin"),
+                 kind="u16", n=64 << 10, nctx=1, fpc=1024, seed=0xA1A8, W=32, golden="cfg4_8192",
+                 layout="roundrobin", params=CFG_ZERO32),
+    "cfg5": dict(desc="configs[4]: 256 streams x 16 acquisitions x 64 Ki i16-in-i32 samples (256 Mi), "
+                      "primary DIFF + GOLOMB_ZERO g=16, secondary MODEL + GOLOMB_MULTI g=8 o=107 rate=11",
+                 kind="i16_in_i32", n=64 << 10, nctx=256, fpc=16, seed=0xA1A9, W=32, golden="cfg5_model",
+                 layout="block",
+                 params=dict(primary_preprocessing=DIFF, primary_encoder_type=ZERO, primary_encoder_param=16,
+                             secondary_iterations=15, secondary_preprocessing=MODEL,
+                             secondary_encoder_type=MULTI, secondary_encoder_param=8,
+                             secondary_encoder_outlier=107, model_rate=11)),
 }
-PARAMS = dict(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=32)
+
+
+def sample_bytes(wl):
+    return 4 if wl["kind"] == "i16_in_i32" else 2
+
+
+def noise_w(wl, f):
+    return (1 << (f % 12)) if wl["W"] == "pow2_mod12" else wl["W"]
+
+
+def algorithmic_bytes(wl):
+    """Compulsory HBM reads of one step: the samples (2 B,
+    or 4 B for i16-in-i32), plus the 2 B model read of every MODEL pass."""
+    n, nf = wl["n"], wl["nctx"] * wl["fpc"]
+    b = nf * n * sample_bytes(wl)
+    if wl["params"].get("secondary_preprocessing") == MODEL:
+        sec = wl["nctx"] * min(wl["fpc"] - 1, wl["params"]["secondary_iterations"])
+        b += sec * n * 2
+    return b
 
 
 def measured_traffic(wname):
-    """HBM bytes per launch of the encode kernel from the latest committed
-    PMC passes (profiles/rNN_traffic_<workload>.json, written by
-    scripts/traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE runs of this
-    bench command), or None."""
+    """HBM bytes per step of the encode path from the latest committed PMC
+    passes (profiles/rNN_traffic_<workload>.json, written by scripts/traffic.py
+    from rocprofv3 FETCH_SIZE / WRITE_SIZE runs of this bench command), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_{wname}.json")))
     if not files:
@@ -71,42 +119,85 @@ def measured_traffic(wname):
 
 
 def frame_ids(wl, rank, world):
+    nf = wl["nctx"] * wl["fpc"]
     if wl["layout"] == "roundrobin":
-        return [rank + world * j for j in range(wl["frames"])]
-    return [rank * wl["frames"] + j for j in range(wl["frames"])]
+        return [rank + world * j for j in range(nf)]
+    return [rank * nf + j for j in range(nf)]
 
 
-def cpu_baseline(wl, threads):
+def host_cpu_info():
+    """CPU resources this job may use: logical CPUs, affinity and the cgroup
+    CPU quota (the GPU box grants a share of a large host)."""
+    info = dict(logical_cpus=os.cpu_count(), affinity=len(os.sched_getaffinity(0)))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            info["cgroup_cpu_quota"] = round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core"):
+                info[k.strip()] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    info["nproc"] = subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip()
+    usable = info["affinity"]
+    if "cgroup_cpu_quota" in info:
+        usable = min(usable, max(1, int(info["cgroup_cpu_quota"])))
+    info["usable_cpus"] = usable
+    return info
+
+
+def cpu_baseline(wl):
     """The reference's own CPU path (oracle/_ref/libref.so, compiled from the
-    reference sources) timed on this host: OpenMP over frames, one context per
-    thread.  Falls back to the clean-room port (oracle/liborc.so)."""
+    reference sources) timed on this host over every CPU this job may use:
+    OpenMP over streams, one context per thread.  Falls back to the clean-room
+    port (oracle/liborc.so) where the reference was not built."""
     api = sys.modules["airs_compression_amd"].cmpapi
     ref = os.path.join(ROOT, "oracle", "_ref", "libref.so")
     orc = os.path.join(ROOT, "oracle", "liborc.so")
     path, kind = (ref, "reference") if os.path.exists(ref) else (orc, "port")
+    cpu = host_cpu_info()
+    threads = cpu["usable_cpus"]
     gen = ctypes.CDLL(orc, mode=ctypes.RTLD_LOCAL)
     gen.orc_synth_u16.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
-    n = wl["n"]
-    nf = min(wl["frames"], 64)
-    data = np.empty((nf, n), dtype=np.uint16)
+    gen.orc_synth_i32.argtypes = gen.orc_synth_u16.argtypes
+    n, sb = wl["n"], sample_bytes(wl)
+    # bounded sample: every frame of cfg2/cfg3/cfg4, 64 of cfg5's 256 streams
+    nctx = min(wl["nctx"], 64)
+    fpc = wl["fpc"]
+    nf = nctx * fpc
+    data = np.empty((nf, n), dtype=np.int32 if sb == 4 else np.uint16)
     for j, f in enumerate(frame_ids(wl, 0, 1)[:nf]):
-        gen.orc_synth_u16(wl["seed"], f, n, wl["W"], data[j].ctypes.data)
+        (gen.orc_synth_i32 if sb == 4 else gen.orc_synth_u16)(wl["seed"], f, n, noise_w(wl, f), data[j].ctypes.data)
     drv = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
     drv.drv_run.restype = ctypes.c_uint64
+    drv.drv_run_autorice.restype = ctypes.c_uint64
     lib = api.CmpLib(path)
     cap = lib.compress_bound(2 * n)
     cap = cap if not api.is_error(cap) else 3 * 2 * n + 64
     stride = (cap + 7) // 8 * 8
     dst = api.aligned_empty(stride * nf)
     sizes = np.zeros(nf, dtype=np.uint32)
-    prm = api.CmpParams(**PARAMS)
+    prm = api.CmpParams(**wl["params"])
+    k_of = {"u16": 0, "i16": 1, "i16_in_i32": 2}[wl["kind"]]
 
     def run(th):
         t0 = time.perf_counter()
-        tot = drv.drv_run(ctypes.byref(prm), 0, ctypes.c_void_p(data.ctypes.data), ctypes.c_uint32(2 * n),
-                          ctypes.c_uint64(2 * n), ctypes.c_uint32(nf), ctypes.c_uint32(1),
-                          ctypes.c_void_p(dst.ctypes.data), ctypes.c_uint64(stride), ctypes.c_uint32(cap),
-                          ctypes.c_void_p(sizes.ctypes.data), ctypes.c_int(th), ctypes.c_int(1))
+        if wl.get("auto_rice"):
+            tot = drv.drv_run_autorice(ctypes.byref(prm), k_of, ctypes.c_void_p(data.ctypes.data),
+                                       ctypes.c_uint32(sb * n), ctypes.c_uint64(sb * n), ctypes.c_uint32(nf),
+                                       ctypes.c_void_p(dst.ctypes.data), ctypes.c_uint64(stride), ctypes.c_uint32(cap),
+                                       ctypes.c_void_p(sizes.ctypes.data), None, ctypes.c_int(th), ctypes.c_int(1))
+        else:
+            tot = drv.drv_run(ctypes.byref(prm), k_of, ctypes.c_void_p(data.ctypes.data), ctypes.c_uint32(sb * n),
+                              ctypes.c_uint64(sb * n), ctypes.c_uint32(nctx), ctypes.c_uint32(fpc),
+                              ctypes.c_void_p(dst.ctypes.data), ctypes.c_uint64(stride), ctypes.c_uint32(cap),
+                              ctypes.c_void_p(sizes.ctypes.data), ctypes.c_int(th), ctypes.c_int(1))
         dt = time.perf_counter() - t0
         assert tot != 2**64 - 1
         return dt
@@ -114,16 +205,71 @@ def cpu_baseline(wl, threads):
     run(threads)  # warm-up
     times = sorted(run(threads) for _ in range(5))
     best = times[0]
-    single = run(1) if nf <= 16 else None
-    nbytes = nf * 2 * n
+    nbytes = nf * sb * n
+    single_nf = max(1, nf // 16)  # single-thread leg on a slice (bounded time)
     out = dict(value=round(nbytes / best / 1e9, 4), unit="GB/s", cores=threads, kind=kind,
-               sample=f"{nf} frames x {n} u16 samples ({nbytes / 2**20:.0f} MiB, the same synthetic frames "
-                      f"and parameters), best of 5 after a warm-up, OpenMP over frames, one context per "
-                      f"thread; host has {os.cpu_count()} logical CPUs",
-               median_value=round(nbytes / times[2] / 1e9, 4))
-    if single is not None:
-        out["single_thread_value"] = round(nbytes / single / 1e9, 4)
+               sample=f"{nf} frames x {n} samples ({nbytes / 2**20:.0f} MiB of {wl['kind']} input, the same "
+                      f"synthetic frames and parameters as the GPU workload), best of 5 after a warm-up, "
+                      f"OpenMP over {'frames' if wl.get('auto_rice') else 'streams'}, one context per thread",
+               median_value=round(nbytes / times[2] / 1e9, 4), host=cpu,
+               cores_note=(f"{threads} threads = every CPU this job may use: the GPU box's cgroup grants "
+                           f"{cpu.get('cgroup_cpu_quota', 'no')} CPUs of the host's {cpu['logical_cpus']} "
+                           f"logical CPUs"))
+    # single thread on the first 1/16 of the frames
+    if not wl.get("auto_rice"):
+        nctx1 = max(1, nctx // 16) if nctx > 1 else 1
+        fpc1 = fpc if nctx > 1 else max(1, fpc // 16)
+        t0 = time.perf_counter()
+        tot = drv.drv_run(ctypes.byref(prm), k_of, ctypes.c_void_p(data.ctypes.data), ctypes.c_uint32(sb * n),
+                          ctypes.c_uint64(sb * n), ctypes.c_uint32(nctx1), ctypes.c_uint32(fpc1),
+                          ctypes.c_void_p(dst.ctypes.data), ctypes.c_uint64(stride), ctypes.c_uint32(cap),
+                          ctypes.c_void_p(sizes.ctypes.data), ctypes.c_int(1), ctypes.c_int(1))
+        dt = time.perf_counter() - t0
+        assert tot != 2**64 - 1
+        single_nf = nctx1 * fpc1
+    else:
+        t0 = time.perf_counter()
+        tot = drv.drv_run_autorice(ctypes.byref(prm), k_of, ctypes.c_void_p(data.ctypes.data),
+                                   ctypes.c_uint32(sb * n), ctypes.c_uint64(sb * n), ctypes.c_uint32(single_nf),
+                                   ctypes.c_void_p(dst.ctypes.data), ctypes.c_uint64(stride), ctypes.c_uint32(cap),
+                                   ctypes.c_void_p(sizes.ctypes.data), None, ctypes.c_int(1), ctypes.c_int(1))
+        dt = time.perf_counter() - t0
+        assert tot != 2**64 - 1
+    out["single_thread_value"] = round(single_nf * sb * n / dt / 1e9, 4)
     return out
+
+
+class BufferSet:
+    """Device buffers of one copy of the workload: inputs, outputs, sizes,
+    contexts (and their device work buffers)."""
+
+    def __init__(self, torch, pkg, lib, eng, wl, fids):
+        api = pkg.cmpapi
+        n, sb = wl["n"], sample_bytes(wl)
+        self.nctx, self.fpc = wl["nctx"], wl["fpc"]
+        nf = self.nctx * self.fpc
+        self.stride = n * sb
+        self.src = torch.empty(nf * self.stride, dtype=torch.uint8, device="cuda")
+        if wl["W"] == "pow2_mod12" or wl["layout"] == "roundrobin":
+            for j, f in enumerate(fids):
+                assert eng.synthesize(self.src.data_ptr() + j * self.stride, sb, wl["seed"], f, n, 1, self.stride,
+                                      noise_w(wl, f)) == 0
+        else:
+            assert eng.synthesize(self.src.data_ptr(), sb, wl["seed"], fids[0], n, nf, self.stride, wl["W"]) == 0
+        cap = lib.compress_bound(2 * n)
+        self.cap = cap if not api.is_error(cap) else 3 * 2 * n + 64
+        self.dstride = (self.cap + 7) // 8 * 8
+        self.dst = torch.empty(nf * self.dstride, dtype=torch.uint8, device="cuda")
+        self.sizes = torch.zeros(nf, dtype=torch.int32, device="cuda")
+        prm = api.CmpParams(**wl["params"])
+        wbs = lib.cal_work_buf_size(prm, self.stride)
+        wstride = (wbs + 15) // 16 * 16
+        self.work = torch.zeros(max(self.nctx * wstride, 16), dtype=torch.uint8, device="cuda")
+        self.ctxs = pkg.context_array(self.nctx)
+        for c in range(self.nctx):
+            r = lib.initialise(self.ctxs[c], prm, (self.work.data_ptr() + c * wstride) if wbs else None, wbs)
+            assert not api.is_error(r), api.error_name(r)
+        self.nbytes = self.src.numel() + self.dst.numel() + self.work.numel()
 
 
 def main():
@@ -132,6 +278,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None)
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="buffer sets to rotate over (0: enough to exceed the 256 MiB Infinity Cache)")
+    ap.add_argument("--no-warm", action="store_true", help="skip the warm (one buffer set) replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     args = ap.parse_args()
@@ -170,66 +319,60 @@ def main():
 
     wname = args.workload or ("cfg2" if world == 1 else "cfg4")
     wl = WORKLOADS[wname]
-    n, nf = wl["n"], wl["frames"]
+    if world > 1 and wl["layout"] != "roundrobin":
+        raise SystemExit(f"--workload {wname} is a single-GPU config; N > 1 runs cfg4 (round-robin frames)")
+    n, nctx, fpc = wl["n"], wl["nctx"], wl["fpc"]
+    nf = nctx * fpc
+    sb = sample_bytes(wl)
     fids = frame_ids(wl, rank, world)
-    stride = 2 * n
-    src = torch.empty(nf * stride, dtype=torch.uint8, device="cuda")
-    if wl["layout"] == "block":
-        assert eng.synthesize(src.data_ptr(), 2, wl["seed"], fids[0], n, nf, stride, wl["W"]) == 0
-    else:
-        for j, f in enumerate(fids):
-            assert eng.synthesize(src.data_ptr() + j * stride, 2, wl["seed"], f, n, 1, stride, wl["W"]) == 0
-    cap = lib.compress_bound(2 * n)
-    cap = cap if not api.is_error(cap) else 3 * 2 * n + 64
-    dstride = (cap + 7) // 8 * 8
-    dst = torch.empty(nf * dstride, dtype=torch.uint8, device="cuda")
-    sizes = torch.zeros(nf, dtype=torch.int32, device="cuda")
-    ctxs = pkg.context_array(1)
-    prm = api.CmpParams(**PARAMS)
-    assert not api.is_error(lib.initialise(ctxs[0], prm))
+    flags = 1 if wl.get("auto_rice") else 0
 
-    def step():
-        r = eng.compress(ctxs, nf, "u16", src.data_ptr(), stride, stride, dst.data_ptr(), dstride, cap,
-                         sizes.data_ptr())
+    sets = [BufferSet(torch, pkg, lib, eng, wl, fids)]
+    rot = args.rotate or max(1, math.ceil(1.25 * INFINITY_CACHE / sets[0].nbytes))
+    rot = max(rot, 3) if sets[0].src.numel() < INFINITY_CACHE else rot
+    for _ in range(rot - 1):
+        sets.append(BufferSet(torch, pkg, lib, eng, wl, fids))
+    torch.cuda.synchronize()
+
+    def step(bs):
+        r = eng.compress(bs.ctxs, fpc, wl["kind"], bs.src.data_ptr(), bs.stride, bs.stride, bs.dst.data_ptr(),
+                         bs.dstride, bs.cap, bs.sizes.data_ptr(), flags)
         if r:
             raise RuntimeError("cmp_gpu_compress: " + api.error_name(r))
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+    def timed(bsets, steps, warmup):
+        for i in range(warmup):
+            step(bsets[i % len(bsets)])
+        torch.cuda.synchronize()
+        # one HIP event pair around the K steps (on the engine's stream): a
+        # pair per step would itself add ~8 us of stream time per step
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for i in range(steps):
+            step(bsets[i % len(bsets)])
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        barrier()
+        wall = time.perf_counter() - t0
+        return wall, ev0.elapsed_time(ev1) / steps
 
-    # one HIP event pair around the K launches (on the engine's stream): a
-    # pair per launch would itself add ~8 us of stream time per step
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for k in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    wall = time.perf_counter() - t0
-    kern_avg_ms = ev0.elapsed_time(ev1) / args.steps
+    wall, kern_avg_ms = timed(sets, args.steps, args.warmup)
     t = torch.tensor([wall], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
+    warm = None
+    if not args.no_warm and world == 1:
+        wwall, wkern = timed(sets[:1], args.steps, 2)
+        warm = dict(value=round(nf * sb * n * args.steps / wwall / 1e9, 3), ms_per_step=round(wwall / args.steps * 1e3, 5),
+                    avg_step_gpu_ms=round(wkern, 5),
+                    note="same K steps replayed on ONE buffer set (inputs may be served by the Infinity Cache)")
 
-    # ---- bit-exactness against the reference's golden digests -------------
-    sz = sizes.cpu().numpy().astype(np.uint32)
-    errs = [api.error_name(int(s)) for s in sz if api.is_error(int(s))]
-    if errs:
-        raise RuntimeError(f"frame errors: {errs[:4]}")
-    host = dst.cpu().numpy()
-    h = hashlib.sha256()
-    for j in range(nf):
-        b = bytearray(host[j * dstride:j * dstride + int(sz[j])])
-        b[8:14] = b"\0" * 6
-        h.update(b)
-    digest = h.hexdigest()
+    # ---- bit-exactness against the reference's golden digests (every set) --
     with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
         gold = json.load(f)["configs"][wl["golden"]]
     key = f"shard_digests_n{world}" if wl["layout"] == "roundrobin" else None
@@ -239,15 +382,30 @@ def main():
         want = gold["digest"]
     else:
         want = None
-    bitexact = (digest == want) if want else None
-    comp_bytes = int(sz.astype(np.uint64).sum())
+    bitexact = None
+    comp_bytes = 0
+    for bs in sets:
+        sz = bs.sizes.cpu().numpy().astype(np.uint32)
+        errs = [api.error_name(int(s)) for s in sz if api.is_error(int(s))]
+        if errs:
+            raise RuntimeError(f"frame errors: {errs[:4]}")
+        host = bs.dst.cpu().numpy()
+        h = hashlib.sha256()
+        for j in range(nf):
+            b = bytearray(host[j * bs.dstride:j * bs.dstride + int(sz[j])])
+            b[8:14] = b"\0" * 6
+            h.update(b)
+        ok = (h.hexdigest() == want) if want else None
+        bitexact = ok if bitexact is None else (bitexact and ok)
+        comp_bytes = int(sz.astype(np.uint64).sum())
+        del host
 
-    # ---- gather of compressed frames to rank 0 over RCCL (not in `value`) --
+    # ---- gather of compressed frames to rank 0 (not in `value`) -----------
     gather = None
     if world > 1 and not args.no_gather:
-        layout = "roundrobin" if wl["layout"] == "roundrobin" else "block"
-        gather, g = pkg.shard.gather_frames_timed(dist, dst, dstride, sizes, nf, rank, world, layout=layout,
-                                                  patch_base=0)
+        bs = sets[0]
+        gather, g = pkg.shard.gather_frames_timed(dist, bs.dst, bs.dstride, bs.sizes, nf, rank, world,
+                                                  layout="roundrobin", patch_base=0)
         if g is not None:
             host_all = g.data.cpu().numpy()
             offs, lens = g.offsets.numpy(), g.sizes.numpy()
@@ -260,22 +418,30 @@ def main():
                 if not ok_id:
                     gather["identifier_patch_ok"] = False
             gather.setdefault("identifier_patch_ok", True)
-            gwant = gold.get(f"gather_digest_n{world}") if wl["layout"] == "roundrobin" else None
+            gwant = gold.get(f"gather_digest_n{world}")
             gather["bitexact_vs_reference"] = (hg.hexdigest() == gwant) if gwant else None
             del g, host_all
 
-    in_bytes_rank = nf * 2 * n
+    in_bytes_rank = nf * sb * n
+    alg_bytes = algorithmic_bytes(wl)
     total_in = in_bytes_rank * world
     value = total_in * args.steps / wall_max / 1e9
     ms_step = wall_max / args.steps * 1e3
     traffic, traffic_src = measured_traffic(wname)
-    achieved = in_bytes_rank / (kern_avg_ms * 1e-3) / 1e9
+    achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
+    kernels = {
+        "cfg2": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL> (u16, DIFF, GOLOMB_ZERO, Rice): one launch per step",
+        "cfg3": "select_rice_kernel + encode_kernel<2,DIFF,ZERO,Rice,0,FULL> (per-frame g): the step's launches",
+        "cfg4": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL>: one launch per step",
+        "cfg5": "encode_kernel<4,DIFF,ZERO,Rice,STORE> + 15 x encode_kernel<4,MODEL,MULTI,Rice,UPDATE>: 16 "
+                "launches per step (one per acquisition)",
+    }
     result = None
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(wl, threads=min(16, os.cpu_count() or 1))
+                cpu = cpu_baseline(wl)
             except Exception as e:  # report, never hide
                 cpu = dict(error=repr(e))
         result = {
@@ -289,15 +455,20 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u16",
-            "data": "synthetic (counter-hash generator, SURVEY.md 8(d)), resident in HBM",
+            "dtype": wl["kind"],
+            "data": (f"synthetic (counter-hash generator, SURVEY.md 8(d)), resident in HBM, rotated over {len(sets)} "
+                     f"buffer sets ({sum(s.nbytes for s in sets) / 2**20:.0f} MiB > the 256 MiB Infinity Cache): "
+                     f"cold reads"),
             "config": {
                 "workload": wl["desc"],
+                "name": wname,
                 "frames_per_gpu": nf,
                 "samples_per_frame": n,
-                "preprocessing": "DIFF", "encoder": "GOLOMB_ZERO", "golomb_g": 32,
+                "sample_type": wl["kind"],
+                "params": wl["params"],
+                "auto_rice": bool(wl.get("auto_rice")),
                 "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
-                "compression_ratio": round(comp_bytes / in_bytes_rank, 4),
+                "compression_ratio": round(comp_bytes / (nf * 2 * n), 4),
             },
             "bitexact_vs_reference": bitexact,
             "roofline": {
@@ -308,17 +479,23 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "airs::encode_kernel<2,1,1,true> (u16, DIFF, GOLOMB_ZERO, Rice)",
-                "algorithmic_bytes_per_launch": in_bytes_rank,
+                "kernel": kernels[wname],
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "algorithmic_bytes_note": "compulsory HBM reads of one step: 2 B/sample (u16), 4 B/sample "
+                                          "(i16-in-i32), +2 B/sample model read per MODEL pass (SURVEY 8(d))",
                 "avg_launch_ms_hip_events": round(kern_avg_ms, 5),
-                "avg_launch_note": "HIP events around the K back-to-back launches on the engine stream, / K",
+                "avg_launch_note": "HIP events around the K back-to-back steps on the engine stream, / K "
+                                   "(all launches of a step)",
             },
             "cpu_baseline": cpu,
         }
+        if warm:
+            result["warm"] = warm
         if gather:
             result["gather"] = gather
         print(json.dumps(result), flush=True)
     barrier()
+    del sets
     eng.close()
     if world > 1:
         dist.destroy_process_group()

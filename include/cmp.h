@@ -115,7 +115,13 @@ uint32_t cmp_initialise(struct cmp_context *ctx, const struct cmp_params *params
 
 /* Compress one frame.  dst must be 8-byte aligned; returns the frame size in
  * bytes or an error.  src_size is in bytes and must stay constant between
- * resets when MODEL preprocessing is configured. */
+ * resets when MODEL preprocessing is configured.
+ *
+ * Threading: as with the reference, one context per thread is allowed (the
+ * timestamp callback must then be thread-safe).  This build stages host
+ * frames through one process-wide GPU engine, so concurrent calls are
+ * serialised by a lock inside the library; for throughput use the batch API
+ * in cmp_gpu.h, one engine per thread or stream. */
 uint32_t cmp_compress_i16(struct cmp_context *ctx, void *dst, uint32_t dst_capacity,
 			  const int16_t *src, uint32_t src_size);
 /* as cmp_compress_i16() but only the low 16 bits of each 32-bit word are used */

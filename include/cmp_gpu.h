@@ -68,13 +68,21 @@ void cmp_gpu_engine_destroy(struct cmp_gpu_engine *engine);
  * misaligned pointers, bad sizes, invalid contexts).  Per-frame results,
  * including frames cmp_compress_* would reject, land in batch->sizes.
  *
- * When no frame can fail (dst_capacity at least the worst-case frame:
- * 26 bytes + 6 per sample) and no context can fall back to raw storage, the
- * call is asynchronous on the engine's stream.  Otherwise the outcome of
- * frame (c, a) decides the pass of frame (c, a+1), so the call runs one
- * acquisition step at a time and synchronises after each step (and after
- * the step's fallbacks, cmp.c:342-393).  Identifier draws are counted per
- * frame and made at the end, in the loop's order. */
+ * The call is asynchronous on the engine's stream when the outcome of a
+ * frame cannot change the pass of the frames after it: dst_capacity is at
+ * least the worst-case frame (26 bytes + 6 per sample), no context can fall
+ * back to raw storage, and -- where that worst case exceeds the 24-bit
+ * compressed-size field (more than ~2.8 Mi samples, so a frame can fail with
+ * CMP_ERR_HDR_CMP_SIZE_TOO_LARGE) -- no context has secondary passes with
+ * frames_per_ctx > 1.  Otherwise the outcome of frame (c, a) decides the pass
+ * of frame (c, a+1), so the call runs one acquisition step at a time and
+ * synchronises after each step (and after the step's fallbacks,
+ * cmp.c:342-393).  Identifier draws are counted per frame and made at the
+ * end, in the loop's order.
+ *
+ * Frames must not overlap: with more than one frame, src_stride >= src_size
+ * and dst_stride >= min(dst_capacity, worst-case frame), else the call
+ * returns CMP_ERR_GENERIC. */
 uint32_t cmp_gpu_compress(struct cmp_gpu_engine *engine, struct cmp_context *ctx, uint32_t num_ctx,
 			  uint32_t frames_per_ctx, const struct cmp_gpu_batch *batch);
 

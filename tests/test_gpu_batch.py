@@ -63,3 +63,101 @@ def test_batch_fallback_identifiers(prod, eng, orc):
         got = bs.run_batch_gpu(prod, eng, api, params, "u16", n, nctx, fpc, cap, srcs)
         assert got == want
         assert all(r == 16 + 2 * n + 4 for r, _ in want[0])
+
+
+def test_batch_size_field_overflow_vs_call_loop(prod, eng, orc):
+    """4 Mi-sample frames whose worst case exceeds the 24-bit compressed-size
+    field: noise frames fail with HDR_CMP_SIZE_TOO_LARGE even though the
+    capacity holds the worst case, and the reference then does not advance
+    the sequence number (cmp.c:321-338), so with secondary passes the next
+    frame's pass depends on the failure (the batch must take the
+    step-by-step path here)."""
+    import numpy as np
+    P = api.CmpParams
+    rng = np.random.default_rng(11)
+    n, nctx, fpc = 4 << 20, 2, 3
+    params = P(primary_preprocessing=0, primary_encoder_type=2, primary_encoder_param=1,
+               primary_encoder_outlier=24, secondary_iterations=2, secondary_preprocessing=0,
+               secondary_encoder_type=2, secondary_encoder_param=1, secondary_encoder_outlier=24)
+    noise = rng.integers(0, 65536, n).astype(np.uint16)   # ~48 bits/sample: > 2^24 - 1 bytes
+    quiet = np.zeros(n, dtype=np.uint16)
+    srcs = [noise, quiet, quiet, quiet, noise, quiet]
+    cap = 26 + 6 * n
+    want = bs.run_batch_host(orc, api, params, "u16", n, nctx, fpc, cap, srcs)
+    assert api.error_name(want[0][0][0]) == "HDR_CMP_SIZE_TOO_LARGE", want[0][0][0]
+    got = bs.run_batch_gpu(prod, eng, api, params, "u16", n, nctx, fpc, cap, srcs)
+    assert got == want
+
+
+def test_batch_rejects_overlapping_frames(prod, eng):
+    import torch
+    n = 4096
+    src = torch.zeros(2 * n * 2, dtype=torch.uint8, device="cuda")
+    cap = prod.compress_bound(2 * n)
+    dst = torch.zeros(4 * cap, dtype=torch.uint8, device="cuda")
+    sizes = torch.zeros(2, dtype=torch.int32, device="cuda")
+    ctxs = (api.CmpContext * 1)()
+    assert not api.is_error(prod.initialise(ctxs[0], api.CmpParams(primary_preprocessing=1,
+                                                                   primary_encoder_type=1,
+                                                                   primary_encoder_param=4)))
+    # dst_stride below the capacity, then src_stride below the frame size
+    assert api.is_error(eng.compress(ctxs, 2, "u16", src.data_ptr(), 2 * n, 2 * n, dst.data_ptr(), 64, cap,
+                                     sizes.data_ptr()))
+    assert api.is_error(eng.compress(ctxs, 2, "u16", src.data_ptr(), 2 * n - 2, 2 * n, dst.data_ptr(),
+                                     (cap + 7) // 8 * 8, cap, sizes.data_ptr()))
+    assert eng.compress(ctxs, 2, "u16", src.data_ptr(), 2 * n, 2 * n, dst.data_ptr(), (cap + 7) // 8 * 8, cap,
+                        sizes.data_ptr()) == 0
+    assert eng.synchronize() == 0
+
+
+def test_host_api_one_context_per_thread(prod, orc):
+    """cmp_compress_* from several threads, one context each (the reference's
+    threading model): every frame equals the oracle's frame for the
+    same context sequence.  Identifier bytes are masked: the threads draw
+    from one shared counter in a nondeterministic order."""
+    import threading
+    import numpy as np
+    P = api.CmpParams
+    nthreads, frames_per_thread = 8, 12
+    params = [P(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=1 << (t % 7),
+                secondary_iterations=3 if t % 2 else 0, secondary_preprocessing=1, secondary_encoder_type=2,
+                secondary_encoder_param=3 + t, secondary_encoder_outlier=40, checksum_enabled=t % 3 == 0)
+              for t in range(nthreads)]
+    rng = np.random.default_rng(3)
+    inputs = [[(np.cumsum(rng.integers(-20, 21, 3000 + 97 * t)) & 0xFFFF).astype(np.uint16)
+               for _ in range(frames_per_thread)] for t in range(nthreads)]
+
+    def run(lib, t, out):
+        ctx = api.CmpContext()
+        assert not api.is_error(lib.initialise(ctx, params[t]))
+        for x in inputs[t]:
+            cap = lib.compress_bound(x.nbytes)
+            dst = api.aligned_empty(cap)
+            r = lib.compress_u16(ctx, dst, cap, x)
+            b = bytearray(dst[:r]) if not api.is_error(r) else None
+            if b is not None:
+                b[8:14] = b"\0" * 6
+            out.append((r, bytes(b) if b is not None else None))
+
+    want = []
+    for t in range(nthreads):
+        w = []
+        run(orc, t, w)
+        want.append(w)
+    got = [[] for _ in range(nthreads)]
+    errs = []
+
+    def worker(t):
+        try:
+            run(prod, t, got[t])
+        except Exception as e:  # reported below
+            errs.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=120)
+    assert not errs, errs
+    for t in range(nthreads):
+        assert got[t] == want[t], f"thread {t} differs from the oracle"

@@ -119,12 +119,16 @@ def test_decode_rejects(eng, orc):
     trunc[2:5] = (200).to_bytes(3, "big")
     model = bytearray(good)
     model[15] = (3 << 4) | (model[15] & 0x0F)  # MODEL preprocessing: needs the model, not decoded
-    frames = [good, bytes(bad_hdr), bytes(trunc), bytes(model)]
+    unknown = [bytearray(good) for _ in range(12)]  # preprocessing 4..15: no such method
+    for p, u in zip(range(4, 16), unknown):
+        u[15] = (p << 4) | (u[15] & 0x0F)
+    frames = [good, bytes(bad_hdr), bytes(trunc), bytes(model)] + [bytes(u) for u in unknown]
     status, outs = gpu_decode(eng, frames, 5000, cap=len(good) + 8)
     assert status[0] == 5000 and np.array_equal(outs[0][:5000], x)
     assert api.error_name(status[1]) == "INT_HDR"
     assert api.error_name(status[2]) == "INT_BITSTREAM"
     assert api.error_name(status[3]) == "PARAMS_INVALID"
+    assert [api.error_name(s) for s in status[4:]] == ["INT_HDR"] * 12
 
 
 def test_decode_model_frames(eng, orc):
