@@ -1,11 +1,14 @@
 # build exp/<NAME>/libairscmp.so from the working tree with extra hipcc flags:
-#   build_exp.sh NAME "FLAGS"     (-DAIRS_EXP_ONLY: only the benchmark kernel, seconds to build)
+#   build_exp.sh NAME "FLAGS"     (-DAIRS_EXP_ONLY: only the benchmark kernels, faster to build)
 set -e
 n=$1; f=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$ROOT/exp/$n"
 cd "$ROOT/airs-compression_amd"
 make -s build/cmp_host.o build/decode.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $f -I../include -Icsrc -c csrc/encode.hip -o ../exp/$n/encode.o
-/opt/rocm/bin/hipcc -shared -Wl,-Bsymbolic -Wl,--no-undefined ../exp/$n/encode.o build/decode.o build/cmp_host.o -o ../exp/$n/libairscmp.so
-rm -f ../exp/$n/encode.o
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $f -I../include -Icsrc"
+$H -c csrc/encode.hip -o ../exp/$n/encode.o &
+$H -c csrc/enc_pipe.hip -o ../exp/$n/enc_pipe.o &
+wait
+/opt/rocm/bin/hipcc -shared -Wl,-Bsymbolic -Wl,--no-undefined ../exp/$n/encode.o ../exp/$n/enc_pipe.o build/decode.o build/cmp_host.o -o ../exp/$n/libairscmp.so
+rm -f ../exp/$n/encode.o ../exp/$n/enc_pipe.o

@@ -17,21 +17,26 @@ api = pkg.cmpapi
 lib = pkg.load()
 wl = dict(bench.WORKLOADS[sys.argv[1]])
 if os.environ.get("AIRS_KB_FRAMES"):  # scaling probe: more frames of the same shape (no golden digest)
-    wl["frames"] = int(os.environ["AIRS_KB_FRAMES"])
+    wl["fpc"] = int(os.environ["AIRS_KB_FRAMES"])
 stream = torch.cuda.current_stream()
 eng = lib.engine(stream.cuda_stream)
-n, nf = wl["n"], wl["frames"]
+n, nf = wl["n"], wl["nctx"] * wl["fpc"]
 stride = 2 * n
-src = torch.empty(nf * stride, dtype=torch.uint8, device="cuda")
-for j, f in enumerate(bench.frame_ids(wl, 0, 1)):
-    eng.synthesize(src.data_ptr() + j * stride, 2, wl["seed"], f, n, 1, stride, wl["W"])
+# AIRS_KB_ROT=R: rotate over R input/output buffer sets (R >= 3 reads cold
+# from HBM: the footprint exceeds the 256 MiB Infinity Cache); default 1 (warm)
+ROT = int(os.environ.get("AIRS_KB_ROT", "1"))
+srcs = [torch.empty(nf * stride, dtype=torch.uint8, device="cuda") for _ in range(ROT)]
+for src in srcs:
+    for j, f in enumerate(bench.frame_ids(wl, 0, 1)):
+        eng.synthesize(src.data_ptr() + j * stride, 2, wl["seed"], f, n, 1, stride, wl["W"])
 cap = lib.compress_bound(2 * n)
 cap = cap if not api.is_error(cap) else 3 * 2 * n + 64
 dstride = (cap + 7) // 8 * 8
-dst = torch.empty(nf * dstride, dtype=torch.uint8, device="cuda")
+dsts = [torch.empty(nf * dstride, dtype=torch.uint8, device="cuda") for _ in range(ROT)]
+src, dst = srcs[0], dsts[0]
 sizes = torch.zeros(nf, dtype=torch.int32, device="cuda")
 ctxs = pkg.context_array(1)
-lib.initialise(ctxs[0], api.CmpParams(**bench.PARAMS))
+lib.initialise(ctxs[0], api.CmpParams(**wl["params"]))
 for k in range(10):
     assert eng.compress(ctxs, nf, "u16", src.data_ptr(), stride, stride, dst.data_ptr(), dstride, cap,
                         sizes.data_ptr()) == 0
@@ -42,6 +47,7 @@ for rep in range(5):  # 5 spans of 20 back-to-back launches, one event pair each
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for k in range(20):
+        src, dst = srcs[k % ROT], dsts[k % ROT]
         assert eng.compress(ctxs, nf, "u16", src.data_ptr(), stride, stride, dst.data_ptr(), dstride, cap,
                             sizes.data_ptr()) == 0
     e1.record(stream)
@@ -64,6 +70,6 @@ with open(os.path.join(bench.ROOT, "tests", "golden", "configs.json")) as f:
 want = gold["shard_digests_n1"][0] if wl["layout"] == "roundrobin" else gold["digest"]
 if os.environ.get("AIRS_KB_FRAMES"):
     want = None
-print(json.dumps(dict(workload=sys.argv[1], dbg=os.environ.get("AIRS_DBG", "0"), median_ms=ms[len(ms) // 2],
+print(json.dumps(dict(workload=sys.argv[1], rot=ROT, dbg=os.environ.get("AIRS_DBG", "0"), median_ms=ms[len(ms) // 2],
                       min_ms=ms[0], GBps=round(nf * 2 * n / (ms[len(ms) // 2] * 1e-3) / 1e9, 1),
                       bitexact=(h.hexdigest() == want) if want else None, frames=nf)))
