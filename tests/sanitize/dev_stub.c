@@ -1,0 +1,212 @@
+/*
+ * dev_stub.c -- TEST ONLY.  A host-memory stand-in for the HIP device layer
+ * (airs_dev.h), so that the C host library (cmp_host.c: parameter checks,
+ * the context state machine, the batch planner and its step-by-step
+ * fallback path) and the CLI parser can run under AddressSanitizer and
+ * UndefinedBehaviorSanitizer on a machine without a GPU (SURVEY.md section 5,
+ * sanitizer row).  It does not encode anything: an "encode" writes a
+ * deterministic pseudo-random outcome per frame (a size that fits, or
+ * CMP_ERR_DST_TOO_SMALL) plus a header-shaped first 16 bytes, which is
+ * enough to drive every branch of the planner.  Device memory is malloc'd
+ * host memory, copies are memcpy.  Never linked into the product.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "airs_dev.h"
+
+#define ERRV(code) ((uint32_t)0u - (uint32_t)(code))
+
+struct airs_dev_engine {
+	void *scratch[AIRS_NSLOT];
+	size_t cap[AIRS_NSLOT];
+	uint64_t salt;
+};
+
+static uint64_t mix(uint64_t z)
+{
+	z += 0x9E3779B97F4A7C15ull;
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+	return z ^ (z >> 31);
+}
+
+int airs_dev_available(void)
+{
+	return 1;
+}
+
+const char *airs_dev_last_error(void)
+{
+	return "stub";
+}
+
+struct airs_dev_engine *airs_dev_engine_create(void *stream)
+{
+	(void)stream;
+	return calloc(1, sizeof(struct airs_dev_engine));
+}
+
+void airs_dev_engine_destroy(struct airs_dev_engine *e)
+{
+	if (!e)
+		return;
+	for (int i = 0; i < AIRS_NSLOT; i++)
+		free(e->scratch[i]);
+	free(e);
+}
+
+void *airs_dev_engine_stream(struct airs_dev_engine *e)
+{
+	(void)e;
+	return NULL;
+}
+
+void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes)
+{
+	if (!e || slot < 0 || slot >= AIRS_NSLOT)
+		return NULL;
+	if (bytes > e->cap[slot]) {
+		free(e->scratch[slot]);
+		e->scratch[slot] = malloc(bytes);
+		e->cap[slot] = e->scratch[slot] ? bytes : 0;
+	}
+	return e->scratch[slot];
+}
+
+uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L)
+{
+	if (!e || !L || !L->n || !L->num_frames || !L->status)
+		return ERRV(1u);
+	for (uint32_t j = 0; j < L->num_frames; j++) {
+		const uint32_t f = L->frame_list ? L->frame_list[j] : L->frame_add + j * L->frame_mul;
+		const uint64_t h = mix(e->salt++ ^ ((uint64_t)f << 32) ^ L->n);
+		/* every input byte the kernel would read is read here too */
+		const uint8_t *src = (const uint8_t *)L->src + (uint64_t)f * L->src_stride;
+		volatile uint8_t sink = src[0] ^ src[(uint64_t)L->n * L->sample_bytes - 1u];
+		(void)sink;
+		uint32_t size = 16u + (uint32_t)(h % (3ull * L->n + 8u));
+		uint8_t *dst = (uint8_t *)L->dst + (uint64_t)f * L->dst_stride;
+		if (L->model_mode != AIRS_MODEL_NONE) {
+			uint8_t *m = L->model_ptrs ? (uint8_t *)(uintptr_t)L->model_ptrs[j]
+						   : (uint8_t *)L->model + (uint64_t)(f / (L->model_div ? L->model_div : 1u)) *
+									     L->model_stride;
+			m[0] ^= 1u; /* touch both ends of the model */
+			m[2u * L->n - 1u] ^= 1u;
+		}
+		if (L->checksum_enabled && L->checksums)
+			(void)L->checksums[f];
+		if (L->frame_g)
+			(void)L->frame_g[f];
+		if (size > L->cap) {
+			L->status[f] = ERRV(30u); /* DST_TOO_SMALL */
+		} else {
+			memset(dst, 0, 16);
+			dst[0] = (uint8_t)(size >> 16);
+			dst[1] = (uint8_t)(size >> 8);
+			dst[2] = (uint8_t)size;
+			dst[size - 1u] = 0x5A;
+			L->status[f] = size;
+		}
+		if (L->needed)
+			L->needed[f] = size;
+	}
+	return 0;
+}
+
+uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src, uint64_t src_stride, uint32_t sample_bytes,
+			   uint32_t n, uint32_t num_frames, const uint32_t *frame_list, uint32_t *out)
+{
+	if (!e || !n || !num_frames)
+		return ERRV(1u);
+	for (uint32_t j = 0; j < num_frames; j++) {
+		const uint32_t f = frame_list ? frame_list[j] : j;
+		const uint8_t *s = (const uint8_t *)src + (uint64_t)f * src_stride;
+		out[frame_list ? f : j] = s[0] + s[(uint64_t)n * sample_bytes - 1u];
+	}
+	return 0;
+}
+
+uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
+			      uint32_t sample_bytes, uint32_t n, uint32_t num_frames, uint32_t preprocessing,
+			      uint32_t *out_g)
+{
+	(void)e, (void)src, (void)src_stride, (void)sample_bytes, (void)n, (void)preprocessing;
+	for (uint32_t f = 0; f < num_frames; f++)
+		out_g[f] = 32u;
+	return 0;
+}
+
+uint32_t airs_dev_synth(struct airs_dev_engine *e, void *dst, uint32_t sample_bytes, uint64_t seed, uint32_t frame0,
+			uint32_t n, uint32_t num_frames, uint64_t stride, uint32_t W)
+{
+	(void)e, (void)W;
+	for (uint32_t f = 0; f < num_frames; f++)
+		for (uint32_t i = 0; i < n * sample_bytes; i++)
+			((uint8_t *)dst)[(uint64_t)f * stride + i] = (uint8_t)mix(seed + frame0 + f + i);
+	return 0;
+}
+
+uint32_t airs_dev_patch_ids(struct airs_dev_engine *e, void *dst, uint64_t dst_stride, uint32_t num_frames,
+			    uint32_t frame_add, uint32_t frame_mul, const uint64_t *ids, const uint32_t *status)
+{
+	(void)e;
+	for (uint32_t j = 0; j < num_frames; j++) {
+		const uint32_t f = frame_add + j * frame_mul;
+		if (status && status[f] > ERRV(128u))
+			continue;
+		for (int b = 0; b < 6; b++)
+			((uint8_t *)dst)[(uint64_t)f * dst_stride + 8u + (uint32_t)b] = (uint8_t)(ids[j] >> (40 - 8 * b));
+	}
+	return 0;
+}
+
+uint32_t airs_dev_decode(struct airs_dev_engine *e, const void *src, uint64_t src_stride, uint32_t src_cap,
+			 uint32_t num_frames, uint16_t *dst, uint64_t dst_stride, uint32_t dst_samples,
+			 uint32_t *status, const uint16_t *model, uint64_t model_stride)
+{
+	(void)e, (void)dst, (void)dst_stride, (void)dst_samples, (void)model, (void)model_stride;
+	for (uint32_t f = 0; f < num_frames; f++) {
+		const uint8_t *s = (const uint8_t *)src + (uint64_t)f * src_stride;
+		status[f] = src_cap ? s[0] + 0u * s[src_cap - 1u] : 0u;
+	}
+	return 0;
+}
+
+void *airs_dev_malloc(size_t bytes)
+{
+	return malloc(bytes ? bytes : 1);
+}
+
+void airs_dev_free(void *p)
+{
+	free(p);
+}
+
+uint32_t airs_dev_h2d(struct airs_dev_engine *e, void *dst, const void *src, size_t bytes)
+{
+	(void)e;
+	memcpy(dst, src, bytes);
+	return 0;
+}
+
+uint32_t airs_dev_d2h(struct airs_dev_engine *e, void *dst, const void *src, size_t bytes)
+{
+	(void)e;
+	memcpy(dst, src, bytes);
+	return 0;
+}
+
+uint32_t airs_dev_sync(struct airs_dev_engine *e)
+{
+	(void)e;
+	return 0;
+}
+
+uint32_t airs_dev_memset(struct airs_dev_engine *e, void *dst, int v, size_t bytes)
+{
+	(void)e;
+	memset(dst, v, bytes);
+	return 0;
+}
