@@ -104,6 +104,9 @@ class AirsLib(CmpLib):
         L.cmp_gpu_synthesize.restype = c_uint32
         L.cmp_gpu_decompress.argtypes = [c_void_p, POINTER(GpuDecodeBatch)]
         L.cmp_gpu_decompress.restype = c_uint32
+        L.cmp_gpu_encode_stream.argtypes = [c_void_p, c_uint32, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32,
+                                            c_uint32, c_void_p, c_uint32, c_void_p]
+        L.cmp_gpu_encode_stream.restype = c_uint32
 
     def gpu_available(self) -> bool:
         return bool(self.lib.cmp_gpu_available())
@@ -152,6 +155,14 @@ class GpuEngine:
                            dst=dst_ptr, dst_stride=dst_stride, dst_samples=dst_samples, status=status_ptr,
                            model=model_ptr or None, model_stride=model_stride)
         return self.lib.lib.cmp_gpu_decompress(self.handle, ctypes.byref(b))
+
+    def encode_stream(self, kind: str, src_ptr: int, num_samples: int, preprocessing: int, encoder_type: int,
+                      encoder_param: int, encoder_outlier: int, dst_ptr: int, dst_capacity: int,
+                      size_ptr: int) -> int:
+        """cmp_gpu_encode_stream: one payload-only bit stream (no header) over device pointers."""
+        return self.lib.lib.cmp_gpu_encode_stream(self.handle, KIND_TO_GPU[kind], src_ptr, num_samples,
+                                                  preprocessing, encoder_type, encoder_param, encoder_outlier,
+                                                  dst_ptr, dst_capacity, size_ptr)
 
     def synchronize(self) -> int:
         return self.lib.lib.cmp_gpu_synchronize(self.handle)

@@ -48,6 +48,13 @@ struct airs_launch {
 	uint32_t encoder_param;  /* Golomb g (ignored for UNCOMPRESSED) */
 	uint32_t outlier_param;  /* user outlier (GOLOMB_MULTI) */
 	const uint32_t *frame_g; /* device, optional per-frame g (all powers of two) */
+	/* CMP_GPU_AUTO_RICE (GOLOMB_ZERO): g = 2^k per frame by the build-defined
+	 * rule.  Frames of a few segments choose k inside the
+	 * encode kernel (one read of the samples); otherwise select_rice_kernel
+	 * writes g into frame_g_scratch (device, one word per batch frame) first */
+	uint32_t auto_rice;
+	uint32_t *frame_g_scratch;
+	uint32_t frame_g_frames;  /* batch frames 0 .. frame_g_frames-1 get a g in the scratch */
 
 	/* model (work buffer): batch frame f's model at model + (f / model_div)*model_stride,
 	 * or model_ptrs[j] (device) */
@@ -83,6 +90,14 @@ void *airs_dev_engine_stream(struct airs_dev_engine *e);
 
 /* enqueue one encode launch; returns 0 or a cmp error value (uint32_t)-code */
 uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L);
+
+/* payload-only stream (cmp_gpu_encode_stream): the n samples at src (device)
+ * as ONE bit stream from bit 0 of dst, no header or checksum; *status
+ * (device) = bytes or error value.  NONE/DIFF preprocessing. */
+#define AIRS_STREAM_MAX 89478485u /* 48 bits per sample stay below 2^32 bits */
+uint32_t airs_dev_encode_stream(struct airs_dev_engine *e, const void *src, uint32_t sample_bytes, uint32_t n,
+				uint32_t preprocessing, uint32_t encoder_type, uint32_t encoder_param,
+				uint32_t outlier_param, void *dst, uint32_t cap, uint32_t *status);
 
 /* XXH32 (seed 419764627) over each frame's samples as big-endian 16-bit words */
 uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src, uint64_t src_stride,

@@ -619,6 +619,43 @@ uint32_t cmp_gpu_synchronize(struct cmp_gpu_engine *engine)
 	return airs_dev_sync(engine->dev);
 }
 
+uint32_t cmp_gpu_encode_stream(struct cmp_gpu_engine *engine, enum cmp_gpu_sample_type type, const void *src,
+			       uint32_t num_samples, enum cmp_preprocessing preprocessing,
+			       enum cmp_encoder_type encoder_type, uint32_t encoder_param, uint32_t encoder_outlier,
+			       void *dst, uint32_t dst_capacity, uint32_t *size)
+{
+	const uint32_t bytes = type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
+	uint32_t e, outlier = 0;
+
+	if (!engine || !size)
+		return ERRV(GENERIC);
+	if ((unsigned)type > CMP_GPU_I16_IN_I32)
+		return ERRV(PARAMS_INVALID);
+	if (!src)
+		return ERRV(SRC_NULL);
+	if (num_samples == 0 || num_samples > AIRS_STREAM_MAX)
+		return ERRV(SRC_SIZE_WRONG);
+	if ((uintptr_t)src % bytes) {
+		fprintf(stderr, "airscmp: cmp_gpu_encode_stream: src must be %u-byte aligned\n", bytes);
+		return ERRV(GENERIC);
+	}
+	if (!dst)
+		return ERRV(DST_NULL);
+	if ((uintptr_t)dst & 7u)
+		return ERRV(DST_UNALIGNED);
+	if (is_err(dst_capacity))
+		return ERRV(GENERIC);
+	if (preprocessing != CMP_PREPROCESS_NONE && preprocessing != CMP_PREPROCESS_DIFF)
+		return ERRV(PARAMS_INVALID);
+	/* the encoder's own checks (encoder.c:185-224) */
+	e = coder_resolve(encoder_type, encoder_param, encoder_outlier, &outlier);
+	if (is_err(e))
+		return e;
+	return airs_dev_encode_stream(engine->dev, src, bytes, num_samples, preprocessing, encoder_type,
+				      encoder_type == CMP_ENCODER_UNCOMPRESSED ? 1u : encoder_param, encoder_outlier,
+				      dst, dst_capacity, size);
+}
+
 uint32_t cmp_gpu_synthesize(struct cmp_gpu_engine *engine, void *dst, uint32_t sample_bytes, uint64_t seed,
 			    uint32_t frame0, uint32_t samples_per_frame, uint32_t num_frames, uint64_t stride,
 			    uint32_t noise_w)
@@ -758,9 +795,9 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 		d_g = airs_dev_scratch(dev, SLOT_G, (size_t)nframes_total * 4u);
 		if (!d_g)
 			return ERRV(GENERIC);
-		e = airs_dev_select_rice(dev, b->src, b->src_stride, bytes, n, nframes_total, P->pre, d_g);
-		if (is_err(e))
-			return e;
+		L.auto_rice = 1;
+		L.frame_g_scratch = d_g;
+		L.frame_g_frames = nframes_total;
 	}
 	L.src = b->src;
 	L.src_stride = b->src_stride;
@@ -778,7 +815,6 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 	L.encoder_type = P->enc;
 	L.encoder_param = P->par;
 	L.outlier_param = P->outlier_param;
-	L.frame_g = d_g;
 	L.model_mode = P->model_mode;
 	L.model_rate = prm->model_rate;
 	L.fail_bit = model_fail_bit(cap, n);

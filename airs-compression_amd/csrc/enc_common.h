@@ -67,7 +67,17 @@ struct KArgs {
 	uint32_t img_words; // LDS image size: AIRS_SEG * (longest codeword) / 32 + 4, multiple of 4
 	uint32_t dbg; // ablation switches (AIRS_DBG env, benchmarking only; 0 in production)
 	uint64_t *dbgts; // AIRS_DBG bit 65536 (ablation builds): per-segment timeline
+	// fused per-frame Rice selection (encode_kernel<..., AUTO>): per segment 16
+	// granules, epoch << 32 | sum over its samples of min((m+1) >> k, 16), k = 0..15
+	uint64_t *ktot;
 };
+
+// fused Rice selection: frames of at most AUTO_MAX_SPF segments (the frame's
+// 16 * spf candidate granules are read by one wave in AUTO_MAX_SPF / 4 loads
+// per lane); larger frames take select_rice_kernel first
+#define AUTO_MAX_SPF 32u
+// histogram bins: v = m + 1 in [1, 65536], bin = 8 floor(log2 v) + next 3 bits
+#define AUTO_BINS 129u
 
 // ---------------------------------------------------------------------
 // Golomb coder constants (reference encoder.c:185-224, with
@@ -404,6 +414,12 @@ __device__ __forceinline__ void dbg_stamp(const KArgs &a, uint32_t gseg, uint32_
 // the persistent pipelined kernel (enc_pipe.hip): whole segments of
 // pipe_segn(sample_bytes) samples, no model, NONE or DIFF; k.segs_per_frame /
 // k.num_segs count those segments
+// payload-only streams (enc_stream.hip): one frame of n <= AIRS_STREAM_MAX
+// samples, no header; bit offsets stay below 2^32 at 48 bits per sample
+uint32_t stream_segn(uint32_t sample_bytes);
+void stream_encode(const KArgs &k, uint32_t sample_bytes, uint32_t pre, uint32_t enc, bool rice, bool full,
+		   uint32_t grid, hipStream_t s);
+
 uint32_t pipe_segn(uint32_t sample_bytes);
 uint32_t pipe_encode(const KArgs &k, uint32_t sample_bytes, uint32_t pre, uint32_t enc, bool rice, hipStream_t s);
 

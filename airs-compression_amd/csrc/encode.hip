@@ -40,828 +40,9 @@
 #include "airs_dev.h"
 
 #include "enc_common.h"
+#include "enc_kernel.h"
 
 namespace airs {
-
-// ---------------------------------------------------------------------
-// the encode kernel
-//   W      bytes per input sample (2: u16/i16, 4: i16 in i32)
-//   PRE    NONE / DIFF / MODEL
-//   ENC    UNCOMPRESSED / GOLOMB_ZERO / GOLOMB_MULTI
-//   RICE   Golomb parameter is a power of two (shift instead of divide)
-//   MODEL  0: no model, 1: store samples (primary pass), 2: update (secondary)
-//
-// One workgroup encodes one segment of SEG_CHUNKS(W, MODEL) chunks of 4096
-// samples; lane t owns samples [16t, 16t+16) of every chunk.  All chunk loads
-// are issued up front (32 KiB per workgroup for u16) so HBM sees many bytes in
-// flight per CU.  Phase 1 computes only code lengths, so the segment's bit
-// total and its last 32 bits are published early; phase 2 rebuilds the
-// codewords chunk by chunk into a double-buffered LDS image and stores them
-// once the look-back has produced the segment's frame bit offset.
-// ---------------------------------------------------------------------
-#ifndef AIRS_SEG_CH
-#define AIRS_SEG_CH 4
-#endif
-__host__ __device__ constexpr uint32_t seg_chunks(int W, int MODEL)
-{
-	return (W == 4 || MODEL) ? 2u : AIRS_SEG_CH;
-}
-// LDS chunk images per workgroup: with three, the look-back is evaluated
-// after the third chunk's packing (chunks 0 and 1 are stored late)
-#ifndef AIRS_NIMG
-#define AIRS_NIMG 3
-#endif
-__host__ __device__ constexpr uint32_t seg_images(int W, int MODEL)
-{
-	return (seg_chunks(W, MODEL) >= 4u && !MODEL) ? AIRS_NIMG : 2u;
-}
-
-#ifdef AIRS_EWPE // minimum waves per SIMD the register allocation must allow
-#define AIRS_EWPE_ATTR __attribute__((amdgpu_waves_per_eu(AIRS_EWPE, 8)))
-#else
-#define AIRS_EWPE_ATTR
-#endif
-template <int W, int PRE, int ENC, bool RICE, int MODEL, bool FULL>
-__global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
-{
-	constexpr uint32_t CH = seg_chunks(W, MODEL);
-	constexpr uint32_t SEGN = CH * AIRS_SEG;
-	constexpr uint32_t NPIECE = ENC == ENC_MULTI ? 2 : 1;
-	// Chunk after whose packing the look-back is evaluated.  1: wave 0 issues
-	// the granule loads when chunk 1's packing starts and reads them when it
-	// ends, so they see the predecessors one chunk later than the aggregate
-	// publish (which an earlier poll mostly misses); chunk 0 is stored late.
-	// 0 with a model, whose chunk-0 update needs the bit offset first.
-	constexpr uint32_t NIMG = seg_images(W, MODEL);
-	constexpr uint32_t LBC = (MODEL || CH < 2) ? 0u : NIMG - 1u;
-	constexpr uint32_t RW = EPT * W / 16u; // uint4 per lane per chunk
-	constexpr uint32_t MRW = EPT / 8u;      // uint4 of 16-bit model values per lane per chunk
-	constexpr bool EXT_HDR = !(PRE == PRE_NONE && ENC == ENC_RAW);
-	constexpr uint32_t HDR_BITS = EXT_HDR ? 176u : 128u;
-	// NIMG chunk images in dynamic LDS, a.img_words each (sized per launch from
-	// the longest codeword the pass can emit), each after a 4-word guard
-	extern __shared__ __attribute__((aligned(16))) uint32_t L_dyn[];
-	const uint32_t IMGW = a.img_words + 4u; // words per image incl. guard (multiple of 4)
-	__shared__ uint32_t s_wsum[CH][EWG / 64];
-	__shared__ uint32_t s_misc[8];
-	// Rice/ZERO code table (fast path): entry q' = min(q, 17) holds
-	// {T'[q'], len[q']} with codeword = m + T'[q'] (see rice_table)
-	__shared__ __attribute__((aligned(16))) uint2 s_rice[20];
-
-	const uint32_t tid = threadIdx.x, lane = tid & 63u;
-	if (DBG(16384u)) // ablation: empty kernel
-		return;
-	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform
-
-	// ---- segment id: dispatch order (or an atomic ticket, debug switch) ----
-	uint32_t seg = blockIdx.x;
-	if (DBG(4u)) {
-		if (tid == 0)
-			s_misc[0] = atomicAdd(a.ticket, 1u) - a.ticket_base;
-		__syncthreads();
-		seg = __builtin_amdgcn_readfirstlane(s_misc[0]);
-	}
-	// Frame-interleaved dispatch: consecutive blocks take the same segment
-	// index of consecutive frames.  A frame's segments are still dispatched in
-	// order (a look-back only waits on earlier blocks) while the segments in
-	// flight spread over all frames, keeping each look-back chain short.
-	const uint32_t nfr = a.num_segs / a.segs_per_frame;
-	const uint32_t sif = seg / nfr;
-	const uint32_t lf = seg - sif * nfr;
-	const uint32_t gseg = lf * a.segs_per_frame + sif; // granule slot: frame-major
-	const uint32_t frame =
-		__builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
-	const bool is_first = sif == 0u;
-	const bool is_last = sif + 1u == a.segs_per_frame;
-	const uint32_t n = a.n;
-	dbg_stamp(a, gseg, 0);
-
-	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
-	// PRE_IWT: the residuals are the frame's IWT coefficients, computed into
-	// the work buffer by iwt_frame_kernel (reference preprocess.c:321-353);
-	// the samples themselves are only needed to store the model (MODEL == 1)
-	constexpr bool LOADM = MODEL == 2 || PRE == PRE_IWT;
-	constexpr bool NEEDX = !(PRE == PRE_IWT && MODEL == 0);
-	uint8_t *fmodel = nullptr;
-	if (MODEL || PRE == PRE_IWT)
-		fmodel = a.model_ptrs ? reinterpret_cast<uint8_t *>(a.model_ptrs[lf])
-				      : a.model + (uint64_t)(frame / a.model_div) * a.model_stride;
-	// FULL launches (host-checked): every segment is whole and every frame and
-	// model base is 16-byte aligned, so no per-lane bounds or alignment tests
-	const bool src_al = FULL || ((uintptr_t)fsrc & 15u) == 0;
-	const bool mod_al = (MODEL || PRE == PRE_IWT) ? (FULL || ((uintptr_t)fmodel & 15u) == 0) : true;
-
-	// ---- phase 0: issue every load of the segment -----------------------
-	uint32_t firstc[CH];
-	uint4 raw[CH][RW];
-	uint4 mraw[CH][MRW];
-	uint32_t prevld[CH];
-#pragma unroll
-	for (uint32_t c = 0; c < CH; c++) {
-		firstc[c] = sif * SEGN + c * AIRS_SEG + tid * EPT;
-		const bool full = FULL || firstc[c] + EPT <= n;
-		if (NEEDX && full && src_al) {
-			const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)firstc[c] * W);
-			if (DBG(512u)) { // ablation: no HBM reads (synthetic in-register data)
-#pragma unroll
-				for (uint32_t q = 0; q < RW; q++)
-					raw[c][q] = make_uint4(0x40004000u + tid * 3u + q, 0x40104008u + c, 0x40204010u ^ tid,
-							       0x40304018u + q * 7u);
-			} else {
-#pragma unroll
-				for (uint32_t q = 0; q < RW; q++)
-					raw[c][q] = p[q];
-			}
-		}
-		if (LOADM && full && mod_al) {
-			const uint4 *p = reinterpret_cast<const uint4 *>(fmodel + (size_t)firstc[c] * 2u);
-#pragma unroll
-			for (uint32_t q = 0; q < MRW; q++)
-				mraw[c][q] = p[q];
-		}
-		prevld[c] = 0u;
-		if (PRE == PRE_DIFF && lane == 0u && firstc[c] != 0u && firstc[c] <= n && !(DBG(512u)))
-			prevld[c] = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fsrc)[firstc[c] - 1u]
-					   : reinterpret_cast<const uint32_t *>(fsrc)[firstc[c] - 1u] & 0xFFFFu;
-	}
-
-	// zero both LDS chunk images while the loads are in flight
-	{
-		uint4 *L4 = reinterpret_cast<uint4 *>(L_dyn);
-		for (uint32_t i = tid; i < ((DBG(4096u)) ? 0u : NIMG * IMGW / 4u); i += EWG)
-			L4[i] = make_uint4(0u, 0u, 0u, 0u);
-	}
-
-	const uint32_t gpar = __builtin_amdgcn_readfirstlane(a.frame_g ? a.frame_g[frame] : a.g);
-	const Coder cd = make_coder<ENC>(ENC == ENC_RAW ? 1u : gpar, a.outlier_param);
-
-	// ---- phase 1: residuals, mapped values, code lengths ------------------
-	// Samples are handled as packed 16-bit pairs: DIFF is one v_pk_sub_u16
-	// against the pair shifted by one sample (v_alignbit), ZigZag three
-	// packed ops, and for Rice/ZERO with k <= 11 the code lengths are summed
-	// with packed ops too (length = k + 1 + min((m + 1) >> k, 16)).
-	const bool fastk = ENC == ENC_ZERO && RICE && cd.k <= 11u;
-	if (fastk && tid < 18u)
-		s_rice[tid] = rice_table_entry(tid, cd.k);
-	uint32_t mp[CH][EPT / 2]; // mapped values, two 16-bit per register
-	// Rice/ZERO fast path (AIRS_KEEP_Q): the code-table byte offsets
-	// 8 min(q, 17) of every pair, computed once in phase 1 next to the lengths
-#ifndef AIRS_KEEP_Q
-#define AIRS_KEEP_Q 1
-#endif
-	uint32_t mq[AIRS_KEEP_Q ? CH : 1][EPT / 2];
-	uint32_t nmp[MODEL ? CH : 1][EPT / 2]; // new model values (MODEL)
-	uint32_t T[CH], nv[CH];
-#pragma unroll
-	for (uint32_t c = 0; c < CH; c++) {
-		const uint32_t first = firstc[c];
-		nv[c] = FULL ? (uint32_t)EPT : first >= n ? 0u : min(n - first, (uint32_t)EPT);
-		uint32_t w[EPT / 2]; // sample pairs (x[2j] | x[2j+1] << 16)
-		if (!NEEDX) {
-#pragma unroll
-			for (uint32_t j = 0; j < EPT / 2; j++)
-				w[j] = 0u;
-		} else if (nv[c] == EPT && src_al) {
-			if (W == 2) {
-#pragma unroll
-				for (uint32_t q = 0; q < RW; q++) {
-					w[4 * q] = raw[c][q].x;
-					w[4 * q + 1] = raw[c][q].y;
-					w[4 * q + 2] = raw[c][q].z;
-					w[4 * q + 3] = raw[c][q].w;
-				}
-			} else {
-#pragma unroll
-				for (uint32_t q = 0; q < RW; q++) {
-					w[2 * q] = __builtin_amdgcn_perm(raw[c][q].y, raw[c][q].x, 0x05040100u);
-					w[2 * q + 1] = __builtin_amdgcn_perm(raw[c][q].w, raw[c][q].z, 0x05040100u);
-				}
-			}
-		} else {
-#pragma unroll
-			for (uint32_t j = 0; j < EPT / 2; j++) {
-				uint32_t x2[2];
-#pragma unroll
-				for (uint32_t h = 0; h < 2; h++) {
-					const uint32_t i = first + 2 * j + h;
-					x2[h] = i < n ? (W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fsrc)[i]
-								: reinterpret_cast<const uint32_t *>(fsrc)[i] & 0xFFFFu)
-						      : 0u;
-				}
-				w[j] = x2[0] | x2[1] << 16;
-			}
-		}
-		uint32_t pm[EPT / 2]; // model pairs (MODEL == 2) or IWT coefficient pairs
-		if (LOADM) {
-			if (nv[c] == EPT && mod_al) {
-#pragma unroll
-				for (uint32_t q = 0; q < MRW; q++) {
-					pm[4 * q] = mraw[c][q].x;
-					pm[4 * q + 1] = mraw[c][q].y;
-					pm[4 * q + 2] = mraw[c][q].z;
-					pm[4 * q + 3] = mraw[c][q].w;
-				}
-			} else {
-#pragma unroll
-				for (uint32_t j = 0; j < EPT / 2; j++) {
-					uint32_t x2[2];
-#pragma unroll
-					for (uint32_t h = 0; h < 2; h++) {
-						const uint32_t i = first + 2 * j + h;
-						x2[h] = i < n ? (uint32_t)reinterpret_cast<const uint16_t *>(fmodel)[i] : 0u;
-					}
-					pm[j] = x2[0] | x2[1] << 16;
-				}
-			}
-		}
-		uint32_t wprev = 0u; // pair whose high half is the sample before this lane's first
-		if (PRE == PRE_DIFF) {
-			wprev = __shfl_up(w[EPT / 2 - 1], 1, 64);
-			if (lane == 0u)
-				wprev = prevld[c] << 16;
-		}
-#pragma unroll
-		for (uint32_t j = 0; j < EPT / 2; j++) {
-			uint32_t u;
-			if (PRE == PRE_DIFF)
-				u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
-			else if (PRE == PRE_MODEL)
-				u = unpk(pk(w[j]) - pk(pm[j]));
-			else if (PRE == PRE_IWT)
-				u = pm[j];
-			else
-				u = w[j];
-			mp[c][j] = (DBG(8192u)) ? w[j] : (ENC == ENC_RAW ? u : zigzag_pk(u));
-		}
-		uint32_t t = 0u;
-		if (DBG(64u)) {
-			t = EPT * (cd.k + 1u) + (mp[c][0] & 7u);
-		} else if (fastk && nv[c] == EPT) {
-			u16x2 acc = (u16x2)(0);
-#pragma unroll
-			for (uint32_t j = 0; j < EPT / 2; j++) {
-				const u16x2 v = __builtin_elementwise_add_sat(pk(mp[c][j]), (u16x2)(1));
-				const u16x2 q = v >> (u16x2)((unsigned short)cd.k);
-				acc += __builtin_elementwise_min(q, (u16x2)(16));
-				if (AIRS_KEEP_Q)
-					mq[AIRS_KEEP_Q ? c : 0][j] = unpk(__builtin_elementwise_min(q, (u16x2)(17)) << (u16x2)(3));
-			}
-			t = EPT * (cd.k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
-		} else {
-#pragma unroll
-			for (uint32_t j = 0; j < EPT; j++)
-				t += j < nv[c] ? len_from_m<ENC, RICE>(half16(mp[c][j >> 1], j & 1u), cd) : 0u;
-		}
-		T[c] = t;
-		if (MODEL) {
-#pragma unroll
-			for (uint32_t j = 0; j < EPT / 2; j++) {
-				if (MODEL == 1) {
-					nmp[MODEL ? c : 0][j] = w[j];
-				} else {
-					uint32_t nm2 = 0u;
-#pragma unroll
-					for (uint32_t h = 0; h < 2; h++) {
-						const uint32_t xv = half16(w[j], h), mv = half16(pm[j], h);
-						const int32_t rate = (int32_t)a.model_rate;
-						const int32_t d = a.is_unsigned ? (int32_t)xv : (int32_t)(int16_t)xv;
-						const int32_t mm = a.is_unsigned ? (int32_t)mv : (int32_t)(int16_t)mv;
-						nm2 |= ((uint32_t)((mm * rate + d * (16 - rate)) >> 4) & 0xFFFFu) << (16u * h);
-					}
-					nmp[MODEL ? c : 0][j] = nm2;
-				}
-			}
-		}
-		// Make the packed mapped values opaque: otherwise the compiler keeps
-		// phase 1's per-sample intermediates alive to CSE them with phase 2's
-		// recomputation, which costs ~100 extra VGPRs and halves occupancy.
-#pragma unroll
-		for (uint32_t i = 0; i < EPT / 2; i++)
-			asm volatile("" : "+v"(mp[c][i]));
-		if (AIRS_KEEP_Q) {
-#pragma unroll
-			for (uint32_t i = 0; i < EPT / 2; i++)
-				asm volatile("" : "+v"(mq[AIRS_KEEP_Q ? c : 0][i]));
-		}
-	}
-
-	if (DBG(32768u)) { // ablation: stop after phase 1
-		if (T[0] == 0x12345u && tid == 999u)
-			a.status[0] = mp[0][0] + mp[CH - 1][1];
-		return;
-	}
-	// ---- per-chunk block scans (DPP within waves, LDS across waves) -------
-	uint32_t inc[CH];
-#pragma unroll
-	for (uint32_t c = 0; c < CH; c++) {
-		inc[c] = wave_incl_scan(T[c]);
-		if (lane == 63u)
-			s_wsum[c][wid] = inc[c];
-	}
-
-	// ---- the segment's last 32 bits (wave 3 rebuilds its last chunk) ------
-#ifndef AIRS_LB_WIN
-#define AIRS_LB_WIN 1
-#endif
-	constexpr int LB_WIN = AIRS_LB_WIN; // look-back windows of 64 granules fetched per round
-	uint64_t gv[LB_WIN];
-#pragma unroll
-	for (int w = 0; w < LB_WIN; w++)
-		gv[w] = 0;
-	__syncthreads(); // B1: wave totals visible
-	uint32_t excl[CH], tot[CH], base[CH];
-	uint32_t A = 0u;
-#pragma unroll
-	for (uint32_t c = 0; c < CH; c++) {
-		uint32_t woff = 0u, tt = 0u;
-#pragma unroll
-		for (uint32_t w = 0; w < EWG / 64; w++) {
-			const uint32_t v = s_wsum[c][w];
-			woff += w < wid ? v : 0u;
-			tt += v;
-		}
-		excl[c] = woff + inc[c] - T[c];
-		tot[c] = __builtin_amdgcn_readfirstlane(tt); // LDS-loaded, but block-uniform
-		base[c] = A;
-		A += tt;
-	}
-	const uint32_t first_seg = gseg - sif;
-	uint64_t tv0 = 0; // predecessor's tail granule, fetched early (lane 0 of wave 0)
-	if (wid == 0) {
-		if (lane == 0) {
-			const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
-			gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
-		}
-		dbg_stamp(a, gseg, 1);
-		if (LBC == 0 && !is_first && !(DBG(2u))) {
-			// the first round's windows, newest first: with ~64 segments of a
-			// frame in flight the nearest inclusive prefix is often past 64
-			lb_prefetch<LB_WIN>(a, gv, tv0, gseg, first_seg, lane);
-		}
-	}
-	if (!is_last && wid == EWG / 64 - 1 && !(DBG(8u))) {
-		// the last lanes' streams (>= EPT bits each) combined: lane 63 gets
-		// the chunk's last 32 bits
-		uint64_t acc = 0u;
-		if (fastk && nv[CH - 1] == EPT) {
-			const char *tab = reinterpret_cast<const char *>(s_rice);
-			auto pair = [&](uint32_t j) {
-				u16x2 qa;
-				if (AIRS_KEEP_Q) {
-					qa = pk(mq[AIRS_KEEP_Q ? CH - 1 : 0][j]);
-				} else {
-					const u16x2 v = __builtin_elementwise_add_sat(pk(mp[CH - 1][j]), (u16x2)(1));
-					qa = __builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17)) << (u16x2)(3);
-				}
-#pragma unroll
-				for (uint32_t h = 0; h < 2; h++) {
-					const uint2 e = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
-					acc = (acc << e.y) | (half16(mp[CH - 1][j], h) + e.x);
-				}
-			};
-			// every sample takes >= k + 1 bits, so for k >= 3 the lane's last
-			// 32 bits lie in its last 8 samples: the first pairs are skipped
-			if (EPT >= 16 && cd.k >= 3u) {
-#pragma unroll
-				for (uint32_t j = EPT / 4; j < EPT / 2; j++)
-					pair(j);
-			} else {
-#pragma unroll
-				for (uint32_t j = 0; j < EPT / 2; j++)
-					pair(j);
-			}
-		} else {
-#pragma unroll
-			for (uint32_t j = 0; j < EPT; j++) {
-				const uint32_t m = (mp[CH - 1][j >> 1] >> (16u * (j & 1u))) & 0xFFFFu;
-				uint32_t c1, l1, c2, l2;
-				code_from_m<ENC, RICE>(m, cd, c1, l1, c2, l2);
-				acc = (acc << l1) | c1;
-				if (NPIECE == 2)
-					acc = (acc << l2) | c2;
-			}
-		}
-		// (v, t) = the last min(T, 32) stream bits of a lane run; combining an
-		// earlier run a with a later b is associative: two scan steps cover
-		// four lanes, >= 32 bits for EPT >= 8
-		uint32_t v = (uint32_t)acc, tb = min(T[CH - 1], 32u);
-#pragma unroll
-		for (uint32_t d = 1; d <= 2; d <<= 1) {
-			const uint32_t va = __shfl_up(v, d, 64), ta = __shfl_up(tb, d, 64);
-			if (lane >= d && tb < 32u) {
-				v = (va << tb) | v;
-				tb = min(ta + tb, 32u);
-			}
-		}
-		if (lane == 63u)
-			gran_store(&a.tail[gseg], ((uint64_t)a.epoch << 32) | v);
-	}
-
-	uint32_t last_ne = 0u; // last non-empty chunk
-#pragma unroll
-	for (uint32_t c = 0; c < CH; c++)
-		last_ne = tot[c] ? c : last_ne;
-
-	uint8_t *fdst = a.dst + (uint64_t)frame * a.dst_stride;
-	const uint32_t cap = a.cap;
-	const __amdgpu_buffer_rsrc_t dst_rsrc = __builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(cap & ~3u), 0x00020000);
-	uint32_t P = 0u;
-	uint32_t pred_c = 0u; // (lane 0 of wave 0) bits preceding chunk c in its first dword
-	const uint32_t tot_first = tot[0];
-
-	// Store one chunk image: funnel-shift it to its frame bit offset.  Complete
-	// words go out through a buffer descriptor whose range is the frame's
-	// capacity rounded down to whole words, so the hardware range check drops
-	// exactly the words that would not fit.
-	auto store_chunk = [&](const uint32_t *Lx, uint32_t basex, uint32_t totx, uint32_t predx, bool finalx) {
-		if (!totx)
-			return;
-		const uint32_t Pc = P + basex;
-		const uint32_t r = Pc & 31u, g0 = Pc >> 5;
-		const uint32_t endbit = Pc + totx;
-		const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
-		const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
-		// four words per thread: one 16-byte LDS read + its left neighbour, one
-		// 16-byte buffer store (the image is 16-byte aligned, j a multiple of 4)
-		const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)Lx);
-		const uint32_t nquad = (DBG(2048u)) ? 0u : (nfull >> 2);
-		for (uint32_t p = tid; p < nquad; p += EWG) {
-			const uint32_t j = 4u * p;
-			const u32x4 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + j);
-			const uint32_t hi = j ? Ll[j - 1u] : predx;
-			u32x4 o;
-			o.x = bswap32(__builtin_amdgcn_alignbit(hi, w.x, r));
-			o.y = bswap32(__builtin_amdgcn_alignbit(w.x, w.y, r));
-			o.z = bswap32(__builtin_amdgcn_alignbit(w.y, w.z, r));
-			o.w = bswap32(__builtin_amdgcn_alignbit(w.z, w.w, r));
-			if (!(DBG(1024u))) // ablation: no HBM writes
-				__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
-		}
-		// the last nfull % 4 words: one each for the threads next in turn
-		// (thread 0 when one of them is word 0, the only word that needs
-		// predx, which lives in lane 0 of wave 0)
-		const uint32_t rr = (tid - nquad) & (EWG - 1u);
-		if (rr < (nfull & 3u) && !(DBG(2048u))) {
-			const uint32_t j = 4u * nquad + rr;
-			const uint32_t hi = j ? Ll[j - 1u] : predx;
-			const uint32_t v = __builtin_amdgcn_alignbit(hi, Ll[j], r);
-			if (!(DBG(1024u)))
-				__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + j)), 0, 0);
-		}
-		if (finalx && nfull == J && tid == 0) {
-			// zero-padded final bytes of the payload (reference bitstream_flush)
-			const uint32_t hi = J ? Lx[J - 1u] : predx;
-			const uint32_t v = __builtin_amdgcn_alignbit(hi, Lx[J], r);
-			const uint32_t gw = g0 + J;
-			const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
-			for (uint32_t b = 0; b < nbytes; b++)
-				if (4u * gw + b < cap)
-					fdst[4u * gw + b] = (uint8_t)(v >> (24u - 8u * b));
-		}
-	};
-
-	// ---- phase 2: chunk by chunk: codewords -> LDS image -> HBM -----------
-	// Waves past phase 1 issue ahead of waves of newer segments on the same
-	// SIMD (still in phase 1): the older segment holds LDS and its frame's
-	// look-back chain, so finishing it first shortens residency (measured:
-	// 1-3 % on cfg2 and the cfg4 shard).
-#ifndef AIRS_PRIO_P2
-#define AIRS_PRIO_P2 1
-#endif
-	if (AIRS_PRIO_P2)
-		__builtin_amdgcn_s_setprio(AIRS_PRIO_P2);
-	// rolled loop (keeps register pressure flat): the current chunk's state is
-	// always index 0 of mp/nmp/nv/excl/tot/base/firstc, rotated at the end
-	uint32_t tot_m3 = 0u; // totals of chunks c-3, c-2 (an image is recycled now), c-1
-	uint32_t tot_m2 = 0u;
-	uint32_t tot_m1 = 0u;
-	uint32_t pred_1 = 0u; // (tid 0) last 32 bits of chunk 0, kept for chunk 1's late store
-	uint32_t pred_2 = 0u; // (tid 0) last 32 bits of chunk 1 (four images: chunk 2 is stored late too)
-#ifndef AIRS_CHUNK_UNROLL
-#define AIRS_CHUNK_UNROLL 4
-#endif
-#pragma unroll AIRS_CHUNK_UNROLL
-	for (uint32_t c = 0; c < CH; c++) {
-		uint32_t *Lc = L_dyn + (c % NIMG) * IMGW + 4u;
-		if (LBC >= 1 && c == LBC + 1u && c >= NIMG)
-			__syncthreads(); // chunk 0's image was stored (late) after the last barrier
-		if (c >= NIMG) {
-			// image c%NIMG was last read by chunk c-NIMG's stores (before the
-			// barrier that ended chunk c-1's packing): clear what it used
-			const uint32_t nw = (max(NIMG == 2 ? tot_m2 : tot_m3, tot[0]) + 31u) >> 5;
-			for (uint32_t i = tid; i <= ((DBG(4096u)) ? 0u : nw); i += EWG)
-				Lc[i] = 0u;
-			__syncthreads();
-		}
-#ifndef AIRS_LBP
-#define AIRS_LBP LBC
-#endif
-		if (LBC >= 1 && c == (AIRS_LBP) && wid == 0 && !is_first && !(DBG(2u))) {
-			lb_prefetch<LB_WIN>(a, gv, tv0, gseg, first_seg, lane);
-		}
-		uint32_t ln[NPIECE][EPT]; // piece lengths (kept for the MODEL fail_bit check)
-		{
-			Packer pk1;
-			pk1.init(Lc, excl[0]);
-			if (DBG(32u)) {
-			} else if (fastk && nv[0] == EPT) {
-				// table-driven: byte offsets 8*min(q, 17) of both samples of a
-				// pair come from three packed ops; codeword = m + T'[q']
-				// (all 16 lookups are issued before the first put: the compiler
-				// does not move LDS reads across the packer's ds_or atomics)
-				const char *tab = reinterpret_cast<const char *>(s_rice);
-#pragma unroll
-				for (uint32_t hb = 0; hb < 2; hb++) { // two batches of 8 lookups
-					uint2 te[EPT / 2];
-#pragma unroll
-					for (uint32_t jj = 0; jj < EPT / 4; jj++) {
-						const uint32_t j = hb * (EPT / 4) + jj;
-						u16x2 qa;
-						if (AIRS_KEEP_Q) {
-							qa = pk(mq[0][j]);
-						} else {
-							const u16x2 v = __builtin_elementwise_add_sat(pk(mp[0][j]), (u16x2)(1));
-							qa = __builtin_elementwise_min(v >> (u16x2)((unsigned short)cd.k), (u16x2)(17))
-							     << (u16x2)(3);
-						}
-#pragma unroll
-						for (uint32_t h = 0; h < 2; h++)
-							te[2 * jj + h] = *reinterpret_cast<const uint2 *>(tab + half16(unpk(qa), h));
-					}
-					// both codewords of a pair go in one put when they fit in 32
-					// bits (almost always).  The test is made once per batch for
-					// the whole wave (one ballot, a uniform branch): if any lane
-					// has a longer pair, the whole batch takes two puts per pair.
-					uint32_t mxl = 0u;
-#pragma unroll
-					for (uint32_t i = 0; i < EPT / 2; i += 2)
-						mxl = max(mxl, te[i].y + te[i + 1].y);
-					if (__ballot(mxl > 32u) == 0ull) {
-#pragma unroll
-						for (uint32_t i = 0; i < EPT / 2; i += 2) {
-							const uint32_t j = hb * (EPT / 2) + i;
-							const uint32_t cwa = (mp[0][j >> 1] & 0xFFFFu) + te[i].x;
-							const uint32_t cwb = (mp[0][j >> 1] >> 16) + te[i + 1].x;
-							pk1.put((cwa << te[i + 1].y) | cwb, te[i].y + te[i + 1].y);
-						}
-					} else {
-#pragma unroll
-						for (uint32_t i = 0; i < EPT / 2; i += 2) {
-							const uint32_t j = hb * (EPT / 2) + i;
-							pk1.put((mp[0][j >> 1] & 0xFFFFu) + te[i].x, te[i].y);
-							pk1.put((mp[0][j >> 1] >> 16) + te[i + 1].x, te[i + 1].y);
-						}
-					}
-#pragma unroll
-					for (uint32_t i = 0; i < EPT / 2; i += 2) {
-						const uint32_t j = hb * (EPT / 2) + i;
-						ln[0][j] = te[i].y;
-						ln[0][j + 1] = te[i + 1].y;
-						if (NPIECE == 2) {
-							ln[NPIECE - 1][j] = 0u;
-							ln[NPIECE - 1][j + 1] = 0u;
-						}
-					}
-				}
-			} else {
-#pragma unroll
-				for (uint32_t j = 0; j < EPT; j++) {
-					const uint32_t m = half16(mp[0][j >> 1], j & 1u);
-					uint32_t c1, l1, c2, l2;
-					code_from_m<ENC, RICE>(m, cd, c1, l1, c2, l2);
-					const bool ok = j < nv[0];
-					l1 = ok ? l1 : 0u;
-					pk1.put(ok ? c1 : 0u, l1);
-					ln[0][j] = l1;
-					if (NPIECE == 2) {
-						l2 = ok ? l2 : 0u;
-						pk1.put(ok ? c2 : 0u, l2);
-						ln[NPIECE - 1][j] = l2;
-					}
-				}
-			}
-			pk1.flush();
-		}
-		__syncthreads();
-		uint32_t pred_next = 0u; // last 32 bits of this chunk, for chunk c+1 (tid 0)
-		if (c + 1u < CH && tid == 0 && tot[0] >= 32u) {
-			const uint32_t s0 = tot[0] - 32u, q = s0 >> 5, sh = s0 & 31u;
-			pred_next = sh ? (Lc[q] << sh) | (Lc[q + 1] >> (32u - sh)) : Lc[q];
-		}
-
-		if (c == LBC) {
-			// ---- decoupled look-back (wave 0), overlapped with the packing ----
-			if (wid == 0) {
-#ifdef AIRS_PRIO_LB // experiment: issue priority of the look-back wave
-				__builtin_amdgcn_s_setprio(AIRS_PRIO_LB);
-#endif
-				dbg_stamp(a, gseg, 3);
-				uint32_t Pw = HDR_BITS;
-				if (DBG(2u)) {
-					Pw = HDR_BITS + sif * 37u; // ablation: no look-back (output garbage)
-				} else if (!is_first) {
-					// round 0 uses the granules fetched before packing; every
-					// round covers LB_WIN windows of 64, newest first
-					uint32_t sum = 0u, spins = 0u, lb_rounds = 0u;
-					int64_t j = (int64_t)gseg - 1;
-					int nwin = LB_WIN;
-					bool done = false;
-					while (!done) {
-						lb_rounds++;
-						bool retry = false;
-#pragma unroll
-						for (int w = 0; w < LB_WIN; w++) {
-							if (w >= nwin || done || retry)
-								break;
-							const int64_t idx = j - 64 * w - (int64_t)lane;
-							const bool inr = idx >= (int64_t)first_seg;
-							const uint32_t tag = (uint32_t)(gv[w] >> 32);
-							const bool valid = inr && (tag >> 1) == a.epoch;
-							const bool incl = valid && (tag & 1u);
-							const uint64_t incl_m = __ballot(incl);
-							const uint64_t bad_m = __ballot(inr && !valid);
-							const uint32_t fi =
-								incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
-							const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
-							if (bad_m & need) {
-								// a needed predecessor has not published: re-poll from here
-								j -= 64 * w;
-								retry = true;
-								break;
-							}
-							sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv[w] : 0u);
-							if (incl_m)
-								done = true;
-						}
-						if (done)
-							break;
-						if (retry) {
-							if (++spins > AIRS_SPIN_LIMIT) {
-								// never expected: a predecessor did not publish.  Give up
-								// (output is garbage, the host reports the fault counter)
-								if (lane == 0)
-									atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-								break;
-							}
-							__builtin_amdgcn_s_sleep(1);
-						} else {
-							j -= 64 * nwin;
-						}
-						nwin = LB_WIN;
-#pragma unroll
-						for (int w = 0; w < LB_WIN; w++) {
-							const int64_t idx = j - 64 * w - (int64_t)lane;
-							gv[w] = idx >= (int64_t)first_seg ? gran_load(&a.agg[idx]) : 0ull;
-						}
-					}
-					Pw = sum;
-					if (lane == 0)
-						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (Pw + A));
-					if ((DBG(65536u)) && a.dbgts && lane == 0)
-						a.dbgts[8u * gseg + 5u] = ((uint64_t)spins << 32) | lb_rounds;
-					if ((DBG(256u)) && lane == 0) { // look-back statistics (debug)
-						atomicAdd(a.ticket + 20, 1u);
-						atomicAdd(a.ticket + 21, lb_rounds);
-						atomicAdd(a.ticket + 22, spins);
-					}
-				}
-				if (lane == 0) {
-					uint32_t pred = 0u;
-					if (is_first || (DBG(2u))) {
-						// header bytes 20-21 (low half of the outlier field) share
-						// the first payload dword of a 22-byte header
-						pred = (EXT_HDR && ENC != ENC_RAW) ? (cd.outlier & 0xFFFFu) : 0u;
-					} else {
-						uint64_t tv = tv0;
-						uint32_t spins = 0;
-						for (; (uint32_t)(tv >> 32) != a.epoch; spins++) {
-							if (spins > AIRS_SPIN_LIMIT) {
-								atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-								break;
-							}
-							__builtin_amdgcn_s_sleep(1);
-							tv = gran_load(&a.tail[gseg - 1u]);
-							if (DBG(256u))
-								atomicAdd(a.ticket + 23, 1u);
-						}
-						if ((DBG(65536u)) && a.dbgts)
-							a.dbgts[8u * gseg + 6u] = spins;
-						pred = (uint32_t)tv;
-					}
-					s_misc[1] = Pw;
-					s_misc[2] = pred;
-				}
-				dbg_stamp(a, gseg, 2);
-#ifdef AIRS_PRIO_LB
-				__builtin_amdgcn_s_setprio(AIRS_PRIO_P2);
-#endif
-			}
-			__syncthreads();
-			P = __builtin_amdgcn_readfirstlane(s_misc[1]);
-			const uint32_t seg_pred = __builtin_amdgcn_readfirstlane(s_misc[2]);
-			if (LBC == 0)
-				pred_c = seg_pred;
-			else if (tot_first) // chunk 0 waited for the look-back: store it now
-				store_chunk(L_dyn + 4u, 0u, tot_first, seg_pred, is_last && last_ne == 0u);
-			if (LBC == 2) // so did chunk 1
-				store_chunk(L_dyn + IMGW + 4u, tot_first, tot_m1, pred_1, is_last && last_ne == 1u);
-			if (LBC == 3) { // and, with four images, chunks 1 and 2
-				store_chunk(L_dyn + IMGW + 4u, tot_first, tot_m2, pred_1, is_last && last_ne == 1u);
-				store_chunk(L_dyn + 2u * IMGW + 4u, tot_first + tot_m2, tot_m1, pred_2,
-					    is_last && last_ne == 2u);
-			}
-		}
-
-		if (c >= LBC)
-			store_chunk(Lc, base[0], tot[0], pred_c, is_last && c == last_ne);
-
-		// ---- model update of chunk c (cmp.c:304-311), old model kept for the
-		// samples the reference's loop never reached (see fail_bit) ----------
-		if (MODEL && nv[0]) {
-			uint64_t bpos = (uint64_t)P + base[0] + excl[0];
-			bool all_ok = true;
-			uint32_t okmask = 0u;
-#pragma unroll
-			for (uint32_t j = 0; j < EPT; j++) {
-#pragma unroll
-				for (uint32_t p = 0; p < NPIECE; p++)
-					bpos += ln[p][j];
-				const bool ok = j < nv[0] && bpos <= a.fail_bit;
-				okmask |= ok ? (1u << j) : 0u;
-				all_ok &= ok;
-			}
-			uint16_t *mpp = reinterpret_cast<uint16_t *>(fmodel) + firstc[0];
-			if (all_ok && mod_al) {
-				const uint32_t *q = nmp[0];
-#pragma unroll
-				for (uint32_t r = 0; r < MRW; r++)
-					reinterpret_cast<uint4 *>(mpp)[r] = make_uint4(q[4 * r], q[4 * r + 1], q[4 * r + 2], q[4 * r + 3]);
-			} else {
-#pragma unroll
-				for (uint32_t j = 0; j < EPT; j++)
-					if (okmask & (1u << j))
-						mpp[j] = (uint16_t)(nmp[0][j >> 1] >> (16u * (j & 1u)));
-			}
-		}
-		if (c == 0)
-			pred_1 = pred_next;
-		if (c == 1)
-			pred_2 = pred_next;
-		pred_c = pred_next;
-		// rotate the per-chunk state
-		tot_m3 = tot_m2;
-		tot_m2 = tot_m1;
-		tot_m1 = tot[0];
-#pragma unroll
-		for (uint32_t k = 0; k + 1 < CH; k++) {
-#pragma unroll
-			for (uint32_t i = 0; i < EPT / 2; i++) {
-				mp[k][i] = mp[k + 1][i];
-				if (AIRS_KEEP_Q)
-					mq[AIRS_KEEP_Q ? k : 0][i] = mq[AIRS_KEEP_Q ? k + 1 : 0][i];
-				if (MODEL)
-					nmp[k][i] = nmp[k + 1][i];
-			}
-			nv[k] = nv[k + 1];
-			excl[k] = excl[k + 1];
-			tot[k] = tot[k + 1];
-			base[k] = base[k + 1];
-			firstc[k] = firstc[k + 1];
-		}
-	}
-
-	dbg_stamp(a, gseg, 4);
-	// ---- frame epilogue: checksum, header, status ------------------------
-	if (is_last && tid == 0) {
-		const uint32_t endbit = P + A;
-		const uint32_t payload_bytes = (endbit + 7u) >> 3;
-		const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
-		if (a.checksum) {
-			const uint32_t ck = a.checksums[frame];
-			for (uint32_t b = 0; b < 4u; b++)
-				if (payload_bytes + b < cap)
-					fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
-		}
-		const uint64_t id = a.ids ? a.ids[lf] : a.id_base + (uint64_t)lf * a.id_step;
-		uint32_t h[5];
-		header_words(h, size, 2u * n, id, a.seq, PRE, a.checksum ? 1u : 0u, ENC,
-			     PRE == PRE_MODEL ? a.model_rate : 0u, ENC == ENC_RAW ? 0u : gpar,
-			     ENC == ENC_RAW ? 0u : cd.outlier);
-		const uint32_t hwords = EXT_HDR ? 5u : 4u;
-#pragma unroll
-		for (uint32_t w = 0; w < 5u; w++)
-			if (w < hwords && 4u * w + 4u <= cap)
-				*reinterpret_cast<uint32_t *>(fdst + 4u * w) = bswap32(h[w]);
-		uint32_t st = size;
-		if (size > cap)
-			st = ERRV(E_DST_TOO_SMALL);
-		else if (size > 0xFFFFFFu)
-			st = ERRV(E_HDR_CMP_SIZE_TOO_LARGE);
-		a.status[frame] = st;
-		if (a.needed)
-			a.needed[frame] = size;
-	}
-}
 
 // ---------------------------------------------------------------------
 // Multi-level integer wavelet transform (reference preprocess.c:140-221,
@@ -1490,6 +671,8 @@ struct airs_dev_engine {
 	size_t scratch_cap[AIRS_NSLOT];
 	uint64_t *dbgts; // debug timeline (AIRS_DBG bit 65536)
 	size_t dbgts_n;
+	uint64_t *ktot; // fused Rice selection: 16 candidate granules per segment
+	size_t ktot_cap;
 };
 
 extern "C" int airs_dev_available(void)
@@ -1532,6 +715,7 @@ extern "C" void airs_dev_engine_destroy(struct airs_dev_engine *e)
 	(void)hipFree(e->tail);
 	(void)hipFree(e->ticket);
 	(void)hipFree(e->dbgts);
+	(void)hipFree(e->ktot);
 	for (int i = 0; i < AIRS_NSLOT; i++)
 		(void)hipFree(e->scratch[i]);
 	free(e);
@@ -1559,6 +743,40 @@ extern "C" void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t by
 	return e->scratch[slot];
 }
 
+// Words of one LDS chunk image: the longest codeword (bits per sample) the
+// pass can emit: UNCOMPRESSED 16; ZERO k+17 (escape, and the longest
+// non-escape code) with k = floor(log2 g), 32 when g varies per frame
+// (g = 0 here); MULTI up to 48 (two pieces)
+static uint32_t image_words(uint32_t encoder_type, uint32_t g)
+{
+	uint32_t maxbits = 48u;
+	if (encoder_type == ENC_RAW) {
+		maxbits = 16u;
+	} else if (encoder_type == ENC_ZERO) {
+		uint32_t kk = 15u;
+		if (g) {
+			kk = 0u;
+			while ((2u << kk) <= g && kk < 31u)
+				kk++;
+		}
+		maxbits = kk + 17u < 32u ? kk + 17u : 32u;
+	}
+#ifdef AIRS_IMG_BITS // experiments only: images too small for the worst case
+	maxbits = AIRS_IMG_BITS;
+#endif
+	const uint32_t words = AIRS_SEG * maxbits / 32u + 4u;
+	return (words + 3u) & ~3u;
+}
+
+// launch epoch tag of the look-back granules (never 0: zeroed granules never match)
+static uint32_t next_epoch(airs_dev_engine *e)
+{
+	e->epoch = (e->epoch + 1u) & 0x7FFFFFFFu;
+	if (e->epoch == 0)
+		e->epoch = 1;
+	return e->epoch;
+}
+
 static uint32_t ensure_granules(airs_dev_engine *e, size_t segs)
 {
 	if (segs <= e->gran_cap)
@@ -1580,6 +798,19 @@ static uint32_t ensure_granules(airs_dev_engine *e, size_t segs)
 template <int W, int PRE, int ENC, bool RICE, int MODEL>
 static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t s)
 {
+	if constexpr (ENC == ENC_ZERO && RICE && MODEL == 0 && (PRE == PRE_NONE || PRE == PRE_DIFF)) {
+		if (k.ktot) { // fused per-frame Rice selection
+			size_t lds = (size_t)2u * (k.img_words + 4u) * 4u; // two images (enc_kernel.h NIMG)
+			lds = lds > AUTO_BINS * 64u * 4u ? lds : AUTO_BINS * 64u * 4u; // the histogram
+			if (full)
+				hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true, true>), dim3(grid),
+						   dim3(EWG), lds, s, k);
+			else
+				hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, false, true>), dim3(grid),
+						   dim3(EWG), lds, s, k);
+			return;
+		}
+	}
 #ifndef AIRS_LDS_EXTRA
 #define AIRS_LDS_EXTRA 0
 #endif
@@ -1758,7 +989,7 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 		const char *v = getenv("AIRS_PIPE");
 		pipe_env = v ? atoi(v) : 0;
 	}
-	const bool pipe = pipe_env != 0 && L->model_mode == AIRS_MODEL_NONE &&
+	const bool pipe = pipe_env != 0 && !L->auto_rice && L->model_mode == AIRS_MODEL_NONE &&
 			  (L->preprocessing == PRE_NONE || L->preprocessing == PRE_DIFF) &&
 			  L->n % pipe_segn(L->sample_bytes) == 0u &&
 			  ((uintptr_t)L->src & 15u) == 0u && (L->src_stride & 15u) == 0u;
@@ -1771,6 +1002,32 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	uint32_t r = ensure_granules(e, (size_t)segs);
 	if (r)
 		return r;
+	// CMP_GPU_AUTO_RICE: fused into the encode kernel for frames of a few
+	// segments without a model; otherwise select_rice_kernel writes g first
+	const bool auto_fused = L->auto_rice && !pipe && L->encoder_type == ENC_ZERO &&
+				L->model_mode == AIRS_MODEL_NONE &&
+				(L->preprocessing == PRE_NONE || L->preprocessing == PRE_DIFF) && spf <= AUTO_MAX_SPF;
+	const uint32_t *frame_g = L->frame_g;
+	if (L->auto_rice && !auto_fused && L->encoder_type == ENC_ZERO) {
+		if (!L->frame_g_scratch)
+			return ERRV(E_GENERIC);
+		r = airs_dev_select_rice(e, L->src, L->src_stride, L->sample_bytes, L->n, L->frame_g_frames,
+					 L->preprocessing, L->frame_g_scratch);
+		if (r)
+			return r;
+		frame_g = L->frame_g_scratch;
+	}
+	if (auto_fused) {
+		if (segs * 16u > e->ktot_cap) {
+			HIPCHECK(hipStreamSynchronize(e->stream));
+			(void)hipFree(e->ktot);
+			e->ktot = nullptr;
+			const size_t want = segs * 16u + segs * 8u + 16384u;
+			HIPCHECK(hipMalloc(&e->ktot, want * sizeof(uint64_t)));
+			HIPCHECK(hipMemset(e->ktot, 0, want * sizeof(uint64_t)));
+			e->ktot_cap = want;
+		}
+	}
 
 	KArgs k;
 	memset(&k, 0, sizeof(k));
@@ -1779,7 +1036,8 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	k.model = (uint8_t *)L->model;
 	k.model_ptrs = L->model_ptrs;
 	k.frame_list = L->frame_list;
-	k.frame_g = L->frame_g;
+	k.frame_g = frame_g;
+	k.ktot = auto_fused ? e->ktot : nullptr;
 	k.checksums = L->checksums;
 	k.ids = L->ids;
 	k.status = L->status;
@@ -1811,33 +1069,8 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	k.enc_hdr = L->encoder_type;
 	k.model_rate_hdr = L->model_rate;
 	k.ticket_base = e->ticket_base;
-	{
-		// longest codeword (bits per sample) the pass can emit, which sizes the
-		// two LDS chunk images: UNCOMPRESSED 16; ZERO k+17 (escape, and the
-		// longest non-escape code) with k = floor(log2 g), 32 when g varies per
-		// frame; MULTI up to 48 (two pieces)
-		uint32_t maxbits = 48u;
-		if (L->encoder_type == ENC_RAW) {
-			maxbits = 16u;
-		} else if (L->encoder_type == ENC_ZERO) {
-			uint32_t kk = 15u;
-			if (!L->frame_g && L->encoder_param) {
-				kk = 0u;
-				while ((2u << kk) <= L->encoder_param && kk < 31u)
-					kk++;
-			}
-			maxbits = kk + 17u < 32u ? kk + 17u : 32u;
-		}
-#ifdef AIRS_IMG_BITS // experiments only: images too small for the worst case
-		maxbits = AIRS_IMG_BITS;
-#endif
-		const uint32_t words = AIRS_SEG * maxbits / 32u + 4u;
-		k.img_words = (words + 3u) & ~3u;
-	}
-	e->epoch = (e->epoch + 1u) & 0x7FFFFFFFu;
-	if (e->epoch == 0)
-		e->epoch = 1;
-	k.epoch = e->epoch;
+	k.img_words = image_words(L->encoder_type, (frame_g || auto_fused) ? 0u : L->encoder_param);
+	k.epoch = next_epoch(e);
 	{
 		static int dbg = -1;
 		if (dbg < 0) {
@@ -1857,7 +1090,7 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 		}
 	}
 
-	bool rice = L->frame_g != nullptr ||
+	bool rice = frame_g != nullptr || auto_fused ||
 		    (L->encoder_param && (L->encoder_param & (L->encoder_param - 1u)) == 0u);
 	if (L->preprocessing == PRE_MODEL && L->model_mode != AIRS_MODEL_UPDATE)
 		return ERRV(E_PARAMS_INVALID);
@@ -1875,15 +1108,59 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 		r = pipe_encode(k, L->sample_bytes, L->preprocessing, L->encoder_type, rice, e->stream);
 		if (r)
 			return r;
-	} else if (L->sample_bytes == 2)
-		dispatch_pre<2>(k, L->preprocessing, L->encoder_type, rice, full, L->model_mode, (uint32_t)segs,
-				e->stream);
-	else
-		dispatch_pre<4>(k, L->preprocessing, L->encoder_type, rice, full, L->model_mode, (uint32_t)segs,
-				e->stream);
+	} else {
+		// fused Rice selection: whole groups of 8 frames (XCD-local frames)
+		const uint32_t grid = auto_fused ? (L->num_frames + 7u) / 8u * 8u * spf : (uint32_t)segs;
+		if (L->sample_bytes == 2)
+			dispatch_pre<2>(k, L->preprocessing, L->encoder_type, rice, full, L->model_mode, grid, e->stream);
+		else
+			dispatch_pre<4>(k, L->preprocessing, L->encoder_type, rice, full, L->model_mode, grid, e->stream);
+	}
 	HIPCHECK(hipGetLastError());
 	if (k.dbg & 4u)
 		e->ticket_base += (uint32_t)segs;
+	return 0;
+}
+
+extern "C" uint32_t airs_dev_encode_stream(struct airs_dev_engine *e, const void *src, uint32_t sample_bytes,
+					  uint32_t n, uint32_t preprocessing, uint32_t encoder_type,
+					  uint32_t encoder_param, uint32_t outlier_param, void *dst, uint32_t cap,
+					  uint32_t *status)
+{
+	if (!e || !src || !dst || !status || n == 0 || n > AIRS_STREAM_MAX)
+		return ERRV(E_GENERIC);
+	if ((preprocessing != PRE_NONE && preprocessing != PRE_DIFF) || encoder_type > ENC_MULTI ||
+	    (sample_bytes != 2 && sample_bytes != 4))
+		return ERRV(E_PARAMS_INVALID);
+	const uint32_t segn = stream_segn(sample_bytes);
+	const uint32_t spf = (n + segn - 1u) / segn;
+	uint32_t r = ensure_granules(e, spf);
+	if (r)
+		return r;
+	KArgs k;
+	memset(&k, 0, sizeof(k));
+	k.src = (const uint8_t *)src;
+	k.dst = (uint8_t *)dst;
+	k.status = status;
+	k.agg = e->agg;
+	k.tail = e->tail;
+	k.ticket = e->ticket;
+	k.model_div = 1u;
+	k.frame_mul = 1u;
+	k.n = n;
+	k.segs_per_frame = spf;
+	k.num_segs = spf;
+	k.cap = cap;
+	k.g = encoder_param;
+	k.outlier_param = outlier_param;
+	k.pre_hdr = preprocessing;
+	k.enc_hdr = encoder_type;
+	k.img_words = image_words(encoder_type, encoder_param);
+	k.epoch = next_epoch(e);
+	const bool rice = encoder_param && (encoder_param & (encoder_param - 1u)) == 0u;
+	const bool full = n % segn == 0u && ((uintptr_t)src & 15u) == 0u;
+	stream_encode(k, sample_bytes, preprocessing, encoder_type, rice, full, spf, e->stream);
+	HIPCHECK(hipGetLastError());
 	return 0;
 }
 

@@ -67,6 +67,10 @@ WORKLOADS = {
     "cfg2": dict(desc="configs[1]: 64 Mi u16 samples as 16 frames x 4 Mi, DIFF + GOLOMB_ZERO g=32",
                  kind="u16", n=4 << 20, nctx=1, fpc=16, seed=0xA1A6, W=32, golden="cfg2_64Mi",
                  layout="block", params=CFG_ZERO32),
+    "cfg2s": dict(desc="configs[1] literally: ONE 64 Mi-sample u16 stream, payload only (no header, no 24-bit "
+                       "frame limit: cmp_gpu_encode_stream), DIFF + GOLOMB_ZERO g=32; the cfg2 samples",
+                  kind="u16", n=4 << 20, nctx=1, fpc=16, seed=0xA1A6, W=32, golden="cfg2_stream",
+                  layout="block", stream=True, params=CFG_ZERO32),
     "cfg3": dict(desc="configs[2]: 1024 frames x 64 Ki u16, W_f = 2^(f mod 12), DIFF + GOLOMB_ZERO with "
                       "the per-frame Rice k (CMP_GPU_AUTO_RICE)",
                  kind="u16", n=64 << 10, nctx=1, fpc=1024, seed=0xA1A7, W="pow2_mod12", golden="cfg3_autorice",
@@ -162,6 +166,8 @@ def cpu_baseline(wl):
     orc = os.path.join(ROOT, "oracle", "liborc.so")
     path, kind = (ref, "reference") if os.path.exists(ref) else (orc, "port")
     cpu = host_cpu_info()
+    if wl.get("stream"):
+        return cpu_baseline_stream(wl, path, kind, orc, cpu)
     threads = cpu["usable_cpus"]
     gen = ctypes.CDLL(orc, mode=ctypes.RTLD_LOCAL)
     gen.orc_synth_u16.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
@@ -171,6 +177,13 @@ def cpu_baseline(wl):
     nctx = min(wl["nctx"], 64)
     fpc = wl["fpc"]
     nf = nctx * fpc
+    # one context owning all frames (cfg2, cfg4) is a serial chain in the
+    # reference; its frames are independent data, so the CPU baseline gives
+    # every frame its own context and runs them on all usable CPUs (the
+    # primary passes are identical; identifiers and sequence numbers differ)
+    split = nctx == 1 and fpc > 1 and not wl["params"].get("secondary_iterations")
+    if split:
+        nctx, fpc = nf, 1
     data = np.empty((nf, n), dtype=np.int32 if sb == 4 else np.uint16)
     for j, f in enumerate(frame_ids(wl, 0, 1)[:nf]):
         (gen.orc_synth_i32 if sb == 4 else gen.orc_synth_u16)(wl["seed"], f, n, noise_w(wl, f), data[j].ctypes.data)
@@ -210,7 +223,8 @@ def cpu_baseline(wl):
     out = dict(value=round(nbytes / best / 1e9, 4), unit="GB/s", cores=threads, kind=kind,
                sample=f"{nf} frames x {n} samples ({nbytes / 2**20:.0f} MiB of {wl['kind']} input, the same "
                       f"synthetic frames and parameters as the GPU workload), best of 5 after a warm-up, "
-                      f"OpenMP over {'frames' if wl.get('auto_rice') else 'streams'}, one context per thread",
+                      f"OpenMP over {'frames' if wl.get('auto_rice') or split else 'streams'}, one context per "
+                      f"{'frame' if split else 'thread'}",
                median_value=round(nbytes / times[2] / 1e9, 4), host=cpu,
                cores_note=(f"{threads} threads = every CPU this job may use: the GPU box's cgroup grants "
                            f"{cpu.get('cgroup_cpu_quota', 'no')} CPUs of the host's {cpu['logical_cpus']} "
@@ -237,6 +251,38 @@ def cpu_baseline(wl):
         assert tot != 2**64 - 1
     out["single_thread_value"] = round(single_nf * sb * n / dt / 1e9, 4)
     return out
+
+
+def cpu_baseline_stream(wl, path, kind, orc, cpu):
+    """One payload-only stream is one serial encoder loop on the CPU (the
+    reference's internal encoder API, oracle/ref_payload.c): one thread, on
+    the first 4 of the 16 frames' samples (16 Mi samples)."""
+    gen = ctypes.CDLL(orc, mode=ctypes.RTLD_LOCAL)
+    gen.orc_synth_u16.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    fn = lib.ref_payload_stream if kind == "reference" else lib.orc_payload_stream
+    fn.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [ctypes.c_void_p, ctypes.c_uint32]
+    fn.restype = ctypes.c_uint32
+    n, frames = wl["n"], 4
+    x = np.empty(frames * n, dtype=np.uint16)
+    for f in range(frames):
+        gen.orc_synth_u16(wl["seed"], f, n, wl["W"], x[f * n:].ctypes.data)
+    cap = 3 * frames * n + 64
+    dst = np.zeros(cap + 8, dtype=np.uint8)
+    off = (-dst.ctypes.data) % 8
+    p = wl["params"]
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        r = fn(x.ctypes.data, frames * n, 0, p["primary_preprocessing"], p["primary_encoder_type"],
+               p["primary_encoder_param"], 0, dst.ctypes.data + off, cap)
+        times.append(time.perf_counter() - t0)
+        assert r < 0xFFFFFF00
+    nbytes = x.nbytes
+    return dict(value=round(nbytes / min(times) / 1e9, 4), unit="GB/s", cores=1, kind=kind,
+                sample=f"one stream of {frames * n} u16 samples ({nbytes / 2**20:.0f} MiB, the first 4 of the 16 "
+                       f"cfg2 frames), best of 3, {'oracle/ref_payload.c over the reference encoder' if kind == 'reference' else 'orc_payload_stream'}",
+                host=cpu, cores_note="a single stream is one serial bit-writer loop: one thread")
 
 
 class BufferSet:
@@ -335,6 +381,14 @@ def main():
     torch.cuda.synchronize()
 
     def step(bs):
+        if wl.get("stream"):  # one payload-only stream over all the samples of the set
+            p = wl["params"]
+            r = eng.encode_stream(wl["kind"], bs.src.data_ptr(), nf * n, p["primary_preprocessing"],
+                                  p["primary_encoder_type"], p["primary_encoder_param"], 0, bs.dst.data_ptr(),
+                                  bs.dst.numel() - 64, bs.sizes.data_ptr())
+            if r:
+                raise RuntimeError("cmp_gpu_encode_stream: " + api.error_name(r))
+            return
         r = eng.compress(bs.ctxs, fpc, wl["kind"], bs.src.data_ptr(), bs.stride, bs.stride, bs.dst.data_ptr(),
                          bs.dstride, bs.cap, bs.sizes.data_ptr(), flags)
         if r:
@@ -373,8 +427,9 @@ def main():
                     note="same K steps replayed on ONE buffer set (inputs may be served by the Infinity Cache)")
 
     # ---- bit-exactness against the reference's golden digests (every set) --
-    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
-        gold = json.load(f)["configs"][wl["golden"]]
+    gfile = "streams.json" if wl.get("stream") else "configs.json"
+    with open(os.path.join(ROOT, "tests", "golden", gfile)) as f:
+        gold = json.load(f)["cases" if wl.get("stream") else "configs"][wl["golden"]]
     key = f"shard_digests_n{world}" if wl["layout"] == "roundrobin" else None
     if key and key in gold:
         want = gold[key][rank]
@@ -385,6 +440,15 @@ def main():
     bitexact = None
     comp_bytes = 0
     for bs in sets:
+        if wl.get("stream"):
+            sz0 = int(bs.sizes[:1].cpu().numpy().astype(np.uint32)[0])
+            if api.is_error(sz0):
+                raise RuntimeError("stream error " + api.error_name(sz0))
+            h = hashlib.sha256(bytes(bs.dst[:sz0].cpu().numpy())).hexdigest()
+            ok = h == gold["sha256"]
+            bitexact = ok if bitexact is None else (bitexact and ok)
+            comp_bytes = sz0
+            continue
         sz = bs.sizes.cpu().numpy().astype(np.uint32)
         errs = [api.error_name(int(s)) for s in sz if api.is_error(int(s))]
         if errs:
@@ -431,7 +495,10 @@ def main():
     achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
     kernels = {
         "cfg2": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL> (u16, DIFF, GOLOMB_ZERO, Rice): one launch per step",
-        "cfg3": "select_rice_kernel + encode_kernel<2,DIFF,ZERO,Rice,0,FULL> (per-frame g): the step's launches",
+        "cfg2s": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,-,STREAM>: one launch per step, one look-back chain "
+                 "of 4096 segments",
+        "cfg3": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO> (the per-frame Rice k chosen in-kernel): one "
+                "launch per step",
         "cfg4": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL>: one launch per step",
         "cfg5": "encode_kernel<4,DIFF,ZERO,Rice,STORE> + 15 x encode_kernel<4,MODEL,MULTI,Rice,UPDATE>: 16 "
                 "launches per step (one per acquisition)",

@@ -110,6 +110,26 @@ struct cmp_gpu_decode_batch {
  * headers and repeated until it settles). */
 uint32_t cmp_gpu_decompress(struct cmp_gpu_engine *engine, const struct cmp_gpu_decode_batch *batch);
 
+/*
+ * Payload-only stream: the num_samples samples at src (device) encoded as ONE
+ * bit stream from bit 0 of dst (device, 8-byte aligned), exactly as the
+ * reference's encoder loop writes a frame's payload -- NONE or DIFF
+ * preprocessing (lib/compress/preprocess.c:268-300), cmp_encoder_encode_s16
+ * (lib/compress/encoder.c:327-378), the big-endian bit writer with its
+ * zero-padded flush (lib/common/bitstream_writer.h:124-158, 205-227) -- but
+ * without header, checksum or the 24-bit frame size limit of a frame, and
+ * without a context.  encoder_outlier is used by GOLOMB_MULTI as by
+ * cmp_initialise.  Asynchronous: *size (device) receives the stream's byte
+ * count, or CMP_ERR_DST_TOO_SMALL when it exceeds dst_capacity (the bytes that
+ * fit are written).  num_samples <= 89478485 (bit offsets stay below 2^32 at
+ * the worst case of 48 bits per sample).  Build-defined extension: no
+ * reference counterpart at the public API.
+ */
+uint32_t cmp_gpu_encode_stream(struct cmp_gpu_engine *engine, enum cmp_gpu_sample_type type, const void *src,
+			       uint32_t num_samples, enum cmp_preprocessing preprocessing,
+			       enum cmp_encoder_type encoder_type, uint32_t encoder_param, uint32_t encoder_outlier,
+			       void *dst, uint32_t dst_capacity, uint32_t *size);
+
 /* wait for all work queued on the engine */
 uint32_t cmp_gpu_synchronize(struct cmp_gpu_engine *engine);
 

@@ -1033,6 +1033,40 @@ uint32_t orc_select_rice_k(const void *src, uint32_t n, uint32_t kind, uint32_t 
 	return best;
 }
 
+/* Payload-only stream (checker of cmp_gpu_encode_stream): the n samples as
+ * one bit stream, the frame loop of compress_engine without the header --
+ * NONE/DIFF residuals (preprocess.c:268-300), cmp_encoder_encode_s16
+ * (encoder.c:327-378), the bit writer and its zero-padded flush
+ * (bitstream_writer.h:124-158, 205-227).  kind 0: 16-bit samples, 1: i16 in
+ * i32.  Returns the byte count or an error value. */
+uint32_t orc_payload_stream(const void *src, uint32_t n, uint32_t kind, uint32_t pre, uint32_t enc, uint32_t g,
+			    uint32_t outlier, void *dst, uint32_t cap)
+{
+	struct orc_src s;
+	struct orc_coder c;
+	struct orc_bw w;
+	uint32_t i, e;
+
+	if (pre != CMP_PREPROCESS_NONE && pre != CMP_PREPROCESS_DIFF)
+		return ORC_ERR(PARAMS_INVALID);
+	e = orc_src_init(&s, src, n * (kind ? 4u : 2u), kind ? ORC_I16_IN_I32 : ORC_U16);
+	if (orc_is_err(e))
+		return e;
+	e = orc_coder_init(&c, enc, g, outlier);
+	if (orc_is_err(e))
+		return e;
+	e = orc_bw_open(&w, dst, cap);
+	if (orc_is_err(e))
+		return e;
+	for (i = 0; i < n; i++) {
+		int16_t x = orc_sample(&s, i);
+		int16_t r = (pre == CMP_PREPROCESS_DIFF && i) ? (int16_t)(x - orc_sample(&s, i - 1)) : x;
+
+		orc_code_sample(&w, r, &c);
+	}
+	return orc_bw_flush(&w);
+}
+
 /* ---------------- decoder (round-trip checks only) ---------------- */
 struct orc_br {
 	const uint8_t *p;

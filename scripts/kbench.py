@@ -28,7 +28,7 @@ ROT = int(os.environ.get("AIRS_KB_ROT", "1"))
 srcs = [torch.empty(nf * stride, dtype=torch.uint8, device="cuda") for _ in range(ROT)]
 for src in srcs:
     for j, f in enumerate(bench.frame_ids(wl, 0, 1)):
-        eng.synthesize(src.data_ptr() + j * stride, 2, wl["seed"], f, n, 1, stride, wl["W"])
+        eng.synthesize(src.data_ptr() + j * stride, 2, wl["seed"], f, n, 1, stride, bench.noise_w(wl, f))
 cap = lib.compress_bound(2 * n)
 cap = cap if not api.is_error(cap) else 3 * 2 * n + 64
 dstride = (cap + 7) // 8 * 8
@@ -37,9 +37,10 @@ src, dst = srcs[0], dsts[0]
 sizes = torch.zeros(nf, dtype=torch.int32, device="cuda")
 ctxs = pkg.context_array(1)
 lib.initialise(ctxs[0], api.CmpParams(**wl["params"]))
+flags = 1 if wl.get("auto_rice") else 0
 for k in range(10):
     assert eng.compress(ctxs, nf, "u16", src.data_ptr(), stride, stride, dst.data_ptr(), dstride, cap,
-                        sizes.data_ptr()) == 0
+                        sizes.data_ptr(), flags) == 0
 torch.cuda.synchronize()
 ms = []
 for rep in range(5):  # 5 spans of 20 back-to-back launches, one event pair each
@@ -49,7 +50,7 @@ for rep in range(5):  # 5 spans of 20 back-to-back launches, one event pair each
     for k in range(20):
         src, dst = srcs[k % ROT], dsts[k % ROT]
         assert eng.compress(ctxs, nf, "u16", src.data_ptr(), stride, stride, dst.data_ptr(), dstride, cap,
-                            sizes.data_ptr()) == 0
+                            sizes.data_ptr(), flags) == 0
     e1.record(stream)
     torch.cuda.synchronize()
     ms.append(e0.elapsed_time(e1) / 20)

@@ -1,0 +1,145 @@
+"""CMP_GPU_AUTO_RICE (the build-defined per-frame Rice k of BASELINE config 3)
+against the oracle: k = orc_select_rice_k of the frame, then the oracle's
+GOLOMB_ZERO encoder with g = 2^k.  Frames of up to AUTO_MAX_SPF segments
+choose k inside the encode kernel (frame-major dispatch, 16 candidate granules
+per segment); larger frames go through select_rice_kernel first.  Both paths,
+both sample widths, NONE and DIFF, whole and partial segments, every k from 0
+to 15 (the scale of the noise sweeps it), and frames holding the extreme
+mapped value 65535 (v = 65536, the top histogram bin).  Bit-exact, with the
+clock-derived identifier bytes 8-13 masked (one context: frame f is that
+context's f-th primary pass)."""
+import zlib
+
+import numpy as np
+import pytest
+
+from conftest import load_pkg
+
+pytestmark = pytest.mark.gpu
+api = load_pkg().cmpapi
+P = api.CmpParams
+SEG16 = 4 * 4096  # samples per segment, 16-bit input (4 chunks)
+SEG32 = 2 * 4096  # i16-in-i32 input (2 chunks)
+AUTO_MAX_SPF = 32
+
+
+@pytest.fixture(scope="module")
+def eng(prod):
+    if not prod.gpu_available():
+        pytest.fail("GPU test run without a usable HIP device")
+    e = prod.engine()
+    yield e
+    e.close()
+
+
+def _frames(rng, kind, n, nf, extreme):
+    """nf frames of a random walk / noise mix whose scale sweeps k = 0..15."""
+    out = []
+    for f in range(nf):
+        scale = 2.0 ** rng.uniform(-1, 15.5)
+        walk = rng.random() < 0.5
+        x = rng.laplace(0, scale, n)
+        if walk:
+            x = np.cumsum(x) * 0.05
+        x = np.clip(np.round(x), -32768, 32767).astype(np.int64)
+        if extreme and f % 2 == 0:
+            x[rng.integers(0, n, 3)] = -32768  # NONE: ZigZag 65535
+            if n >= 2:
+                i = int(rng.integers(1, n))
+                x[i - 1], x[i] = 32767, -32768  # DIFF: residual -32768 (wraps) -> 65535 too
+        if kind == "u16":
+            out.append((x & 0xFFFF).astype(np.uint16))
+        elif kind == "i16":
+            out.append(x.astype(np.int16))
+        else:  # i16 in i32: junk in the high half, which the encoder ignores
+            hi = rng.integers(-30000, 30000, n).astype(np.int64) << 16
+            out.append(((x & 0xFFFF) | hi).astype(np.int64).astype(np.int32))
+    return out
+
+
+def _oracle(orc, orc_ext, kind, pre, frames):
+    want = []
+    for x in frames:
+        n = x.size
+        k = orc_ext.orc_select_rice_k(np.ascontiguousarray(x).ctypes.data, n, 1 if kind == "i16_in_i32" else 0,
+                                      pre, None)
+        ctx = api.CmpContext()
+        prm = P(primary_preprocessing=pre, primary_encoder_type=api.ENCODER_GOLOMB_ZERO,
+                primary_encoder_param=1 << k)
+        assert not api.is_error(orc.initialise(ctx, prm))
+        cap = orc.compress_bound(2 * n)
+        dst = api.aligned_empty(cap)
+        r = orc.compress(kind, ctx, dst, cap, x)
+        assert not api.is_error(r), api.error_name(r)
+        want.append(bytes(dst[:r]))
+    return want
+
+
+def _gpu(prod, eng, kind, pre, frames):
+    import torch
+    n, nf = frames[0].size, len(frames)
+    sb = 4 if kind == "i16_in_i32" else 2
+    stride = (n * sb + 15) // 16 * 16  # 16-byte aligned frames (the FULL kernels when n fills segments)
+    host = np.zeros(nf * stride, dtype=np.uint8)
+    for f, x in enumerate(frames):
+        host[f * stride:f * stride + n * sb] = np.ascontiguousarray(x).view(np.uint8)
+    src = torch.from_numpy(host).cuda()
+    cap = prod.compress_bound(2 * n)
+    cap = cap if not api.is_error(cap) else 6 * n + 64
+    dstride = (cap + 7) // 8 * 8
+    dst = torch.full((nf * dstride,), 0xAB, dtype=torch.uint8, device="cuda")
+    sizes = torch.zeros(nf, dtype=torch.int32, device="cuda")
+    ctxs = (api.CmpContext * 1)()
+    # the configured g is ignored by AUTO_RICE (any valid g)
+    prm = P(primary_preprocessing=pre, primary_encoder_type=api.ENCODER_GOLOMB_ZERO, primary_encoder_param=7)
+    assert not api.is_error(prod.initialise(ctxs[0], prm))
+    torch.cuda.synchronize()
+    r = eng.compress(ctxs, nf, kind, src.data_ptr(), stride, n * sb, dst.data_ptr(), dstride, cap,
+                     sizes.data_ptr(), 1)
+    assert r == 0, api.error_name(r)
+    assert eng.synchronize() == 0
+    sz = sizes.cpu().numpy().astype(np.uint32)
+    out = dst.cpu().numpy()
+    got = []
+    for f in range(nf):
+        assert not api.is_error(int(sz[f])), api.error_name(int(sz[f]))
+        got.append(bytes(out[f * dstride:f * dstride + int(sz[f])]))
+    return got
+
+
+def _mask(b):
+    b = bytearray(b)
+    b[8:14] = b"\0" * 6
+    return bytes(b)
+
+
+CASES = []
+for kind, seg in (("u16", SEG16), ("i16", SEG16), ("i16_in_i32", SEG32)):
+    for pre in (0, 1):
+        for n in (1, 7, 4096, seg - 1, seg, 3 * seg + 517, 4 * seg, AUTO_MAX_SPF * seg,
+                  AUTO_MAX_SPF * seg + 100):
+            CASES.append((kind, pre, n))
+
+
+@pytest.mark.parametrize("kind,pre,n", CASES)
+def test_autorice_vs_oracle(prod, eng, orc, orc_ext, kind, pre, n):
+    rng = np.random.default_rng(zlib.crc32(f"{kind}/{pre}/{n}".encode()))
+    budget = 3 << 20  # samples per case (oracle time)
+    nf = int(max(2, min(24, budget // max(n, 1))))
+    frames = _frames(rng, kind, n, nf, extreme=True)
+    want = _oracle(orc, orc_ext, kind, pre, frames)
+    got = _gpu(prod, eng, kind, pre, frames)
+    bad = [f for f in range(nf) if _mask(got[f]) != _mask(want[f])]
+    assert not bad, (f"frames {bad[:8]} differ; g gpu/oracle "
+                     f"{[(api.parse_header(got[f])['encoder_param'], api.parse_header(want[f])['encoder_param']) for f in bad[:4]]}")
+
+
+def test_autorice_k_range(prod, eng, orc, orc_ext):
+    """The sweep reaches every k: scales 2^-1 .. 2^15.5 over 64 frames."""
+    rng = np.random.default_rng(11)
+    frames = _frames(rng, "u16", SEG16, 64, extreme=False)
+    got = _gpu(prod, eng, "u16", 0, frames)
+    want = _oracle(orc, orc_ext, "u16", 0, frames)
+    assert [_mask(g) for g in got] == [_mask(w) for w in want]
+    ks = {api.parse_header(g)["encoder_param"].bit_length() - 1 for g in got}
+    assert len(ks) >= 12, sorted(ks)
