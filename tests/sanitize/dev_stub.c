@@ -115,6 +115,25 @@ uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L)
 	return 0;
 }
 
+uint32_t airs_dev_encode_stream(struct airs_dev_engine *e, const void *src, uint32_t sample_bytes, uint32_t n,
+				uint32_t preprocessing, uint32_t encoder_type, uint32_t encoder_param,
+				uint32_t outlier_param, void *dst, uint32_t cap, uint32_t *status)
+{
+	(void)preprocessing, (void)encoder_type, (void)encoder_param, (void)outlier_param;
+	if (!e || !n)
+		return ERRV(1u);
+	volatile uint8_t sink = ((const uint8_t *)src)[(uint64_t)n * sample_bytes - 1u];
+	(void)sink;
+	const uint32_t size = 1u + (uint32_t)(mix(e->salt++) % (3ull * n));
+	if (size > cap) {
+		*status = ERRV(30u);
+	} else {
+		((uint8_t *)dst)[size - 1u] = 0x5A;
+		*status = size;
+	}
+	return 0;
+}
+
 uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src, uint64_t src_stride, uint32_t sample_bytes,
 			   uint32_t n, uint32_t num_frames, const uint32_t *frame_list, uint32_t *out)
 {

@@ -18,7 +18,8 @@
 
 static uint64_t g_rng;
 /* outcome counters: the run must reach the interesting paths */
-static uint32_t n_init_ok, n_frames_ok, n_frames_err, n_batch_ok, n_batch_frames_ok, n_batch_fallback_cap;
+static uint32_t n_init_ok, n_frames_ok, n_frames_err, n_batch_ok, n_batch_frames_ok, n_batch_fallback_cap,
+	n_stream_ok;
 
 static uint32_t rnd(void)
 {
@@ -166,6 +167,19 @@ static void fuzz_batch(struct cmp_gpu_engine *eng)
 			(void)cmp_gpu_compress(eng, ctx, nctx, fpc, &b);
 		(void)cmp_gpu_synchronize(eng);
 	}
+	/* payload-only stream over the batch's samples */
+	{
+		uint32_t ssz = 0;
+		const uint32_t st = pick(5) ? type : pick(9), ssb = st == 2 ? 4u : 2u;
+		/* at most the samples the batch buffer holds */
+		const uint32_t sn = (uint32_t)(stride * nf / ssb);
+		const uint32_t r = cmp_gpu_encode_stream(eng, (enum cmp_gpu_sample_type)st,
+							 pick(20) ? src : NULL, pick(20) ? 1u + pick(sn) : 0,
+							 (enum cmp_preprocessing)pick(5), (enum cmp_encoder_type)pick(4),
+							 pick(8) ? 1u + pick(70) : pick(70000), pick(300), pick(20) ? dst : NULL,
+							 pick(2) ? cap : (uint32_t)(dstride * nf), &ssz);
+		n_stream_ok += !cmp_is_error(r) && !cmp_is_error(ssz);
+	}
 	/* argument errors */
 	b.dst_stride = pick(2) ? 1 : dstride;
 	b.src_size = pick(2) ? 3 : n * sb;
@@ -226,7 +240,8 @@ int main(int argc, char **argv)
 	}
 	cmp_gpu_engine_destroy(eng);
 	printf("host_fuzz: %u iterations clean: %u contexts initialised, host frames %u ok / %u errors, "
-	       "%u batches (%u frames ok, %u with fallback enabled)\n",
-	       iters, n_init_ok, n_frames_ok, n_frames_err, n_batch_ok, n_batch_frames_ok, n_batch_fallback_cap);
+	       "%u batches (%u frames ok, %u with fallback enabled), %u streams\n",
+	       iters, n_init_ok, n_frames_ok, n_frames_err, n_batch_ok, n_batch_frames_ok, n_batch_fallback_cap,
+	       n_stream_ok);
 	return 0;
 }
