@@ -68,6 +68,7 @@ struct airs_launch {
 	uint64_t fail_bit;       /* samples reaching this frame bit keep their old model */
 
 	/* header fields */
+	const uint8_t *seqs;     /* device, optional: sequence number per batch frame (else seq) */
 	uint64_t id_base;        /* identifier of launch frame j = id_base + j*id_step, or ids[j] */
 	uint64_t id_step;
 	const uint64_t *ids;     /* device, optional */
@@ -98,6 +99,39 @@ uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L)
 uint32_t airs_dev_encode_stream(struct airs_dev_engine *e, const void *src, uint32_t sample_bytes, uint32_t n,
 				uint32_t preprocessing, uint32_t encoder_type, uint32_t encoder_param,
 				uint32_t outlier_param, void *dst, uint32_t cap, uint32_t *status);
+
+/* Batch fallback path on the device (cmp_gpu_compress): per-context state
+ * machine of compress_engine / cmp_compress_generic (cmp.c:228-246, 342-393).
+ * airs_dev_fb_step resolves step `prev` (>= 0) and plans step `cur` (>= 0);
+ * airs_dev_fb_copy writes the raw frames of step `prev`'s fallbacks. */
+struct airs_fb_step {
+	uint32_t *state;          /* device [2 num_ctx]: sequence number, model size */
+	uint32_t num_ctx, fpc;
+	int32_t prev, cur;
+	uint32_t packed;          /* 2 n */
+	uint32_t iters;           /* secondary_iterations */
+	uint32_t model_needed;    /* model_is_needed(params) */
+	uint32_t fb_eligible;     /* fallback enabled and dst_capacity >= raw_size */
+	uint32_t raw_size;        /* header + 2 n (+ checksum) */
+	uint32_t err_floor;       /* values above are errors */
+	uint32_t err_small, err_mismatch, err_too_large;
+	uint32_t *flist_p, *flist_s; /* device [num_ctx]: launch lists of step cur (AIRS_NO_FRAME holes) */
+	uint8_t *seqs, *draws, *kind, *fb; /* device [num frames] */
+	uint32_t *status;         /* device [num frames]: the batch sizes */
+	/* raw frame writer (fb_copy) */
+	const void *src;
+	uint64_t src_stride;
+	uint32_t sample_bytes, n;
+	void *dst;
+	uint64_t dst_stride;
+	const uint32_t *checksums;
+	uint32_t checksum;
+	void *model;              /* strided work buffers (context c at model + c model_stride), or */
+	uint64_t model_stride;
+	const uint64_t *model_ptrs; /* device [num_ctx] */
+};
+uint32_t airs_dev_fb_step(struct airs_dev_engine *e, const struct airs_fb_step *s);
+uint32_t airs_dev_fb_copy(struct airs_dev_engine *e, const struct airs_fb_step *s);
 
 /* XXH32 (seed 419764627) over each frame's samples as big-endian 16-bit words */
 uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src, uint64_t src_stride,

@@ -1009,6 +1009,269 @@ out:
 	return e;
 }
 
+/*
+ * Exact mode on the device.  When every context has the same parameters, no
+ * pass is IWT (its transform is computed per launch into the work buffer)
+ * and the prologue's static checks pass for both passes, the state machine
+ * that batch_exact() steps on the host runs on the GPU instead
+ * (airs_dev_fb_step / airs_dev_fb_copy, airs_dev.h): per acquisition step a
+ * planning kernel, the primary-pass launch, the secondary-pass launch (holes
+ * in their frame lists skip the contexts on the other pass) and the raw
+ * frames of the previous step's fallbacks.  The only host round trip is one
+ * read-back of the identifier draw counts and context states at the end;
+ * identifiers are then drawn in call order and patched into the headers.
+ */
+/* AIRS_HOST_EXACT=1 (tests, comparisons): keep the host-stepped exact mode */
+static int host_exact_forced(void)
+{
+	const char *v = getenv("AIRS_HOST_EXACT");
+
+	return v && atoi(v) != 0;
+}
+
+static int same_params(const struct cmp_params *x, const struct cmp_params *y)
+{
+	return x->primary_preprocessing == y->primary_preprocessing &&
+	       x->primary_encoder_type == y->primary_encoder_type &&
+	       x->primary_encoder_param == y->primary_encoder_param &&
+	       x->primary_encoder_outlier == y->primary_encoder_outlier &&
+	       x->secondary_iterations == y->secondary_iterations &&
+	       x->secondary_preprocessing == y->secondary_preprocessing &&
+	       x->secondary_encoder_type == y->secondary_encoder_type &&
+	       x->secondary_encoder_param == y->secondary_encoder_param &&
+	       x->secondary_encoder_outlier == y->secondary_encoder_outlier && x->model_rate == y->model_rate &&
+	       x->checksum_enabled == y->checksum_enabled &&
+	       x->uncompressed_fallback_enabled == y->uncompressed_fallback_enabled;
+}
+
+/* first-attempt capacity of a frame (cmp_compress_generic, cmp.c:358-366) */
+static uint32_t first_cap(const struct cmp_context *ctx, const struct cmp_gpu_batch *b, uint32_t n)
+{
+	const uint32_t raw = raw_frame_size(ctx, n);
+
+	return ctx->params.uncompressed_fallback_enabled && b->dst_capacity >= raw ? raw : b->dst_capacity;
+}
+
+/* can batch_device_exact() run this batch?  pp / ps receive the two passes */
+static int device_exact_ok(const struct cmp_context *ctx, uint32_t num_ctx, const struct cmp_gpu_batch *b,
+			   uint32_t n, struct pass *pp, struct pass *ps)
+{
+	const struct cmp_params *P = &ctx[0].params;
+	uint32_t c, draws = 0;
+
+	if (P->primary_preprocessing == CMP_PREPROCESS_IWT ||
+	    (P->secondary_iterations && P->secondary_preprocessing == CMP_PREPROCESS_IWT))
+		return 0;
+	for (c = 0; c < num_ctx; c++) {
+		struct cmp_context t;
+		struct pass p;
+
+		if (!same_params(&ctx[c].params, P))
+			return 0;
+		t = ctx[c];
+		t.sequence_number = 0;
+		if (is_err(engine_prologue(&t, b->dst, first_cap(&ctx[c], b, n), n, &p, &draws)))
+			return 0;
+		if (c == 0)
+			*pp = p;
+		if (P->secondary_iterations) {
+			t = ctx[c];
+			t.sequence_number = 1;
+			t.model_size = 2u * n;
+			if (is_err(engine_prologue(&t, b->dst, first_cap(&ctx[c], b, n), n, &p, &draws)))
+				return 0;
+			if (c == 0)
+				*ps = p;
+		}
+	}
+	return 1;
+}
+
+static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx,
+				   uint32_t fpc, const struct cmp_gpu_batch *b, const struct pass *pp,
+				   const struct pass *ps, uint64_t *ids)
+{
+	struct airs_dev_engine *dev = eng->dev;
+	const struct cmp_params *P = &ctx[0].params;
+	const uint32_t bytes = b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
+	const uint32_t n = b->src_size / bytes, total = num_ctx * fpc;
+	const uint32_t cap1 = first_cap(&ctx[0], b, n), mneed = model_needed(P) ? 1u : 0u;
+	const size_t words = 4u * (size_t)num_ctx, tb = ((size_t)total + 15u) & ~(size_t)15u;
+	uint32_t *host_state = calloc(2u * (size_t)num_ctx, sizeof(uint32_t));
+	uint8_t *host_draws = calloc(total, 1);
+	uint8_t *scr = airs_dev_scratch(dev, SLOT_FL, words * 4u + 4u * tb);
+	uint32_t *d_ck = NULL, *d_g = NULL, c, a, e = 0;
+	uint64_t *d_ptr = NULL, mstride = 0;
+	void *mbase = NULL;
+	struct airs_fb_step S;
+
+	if (!host_state || !host_draws || !scr) {
+		e = ERRV(GENERIC);
+		goto out;
+	}
+	memset(&S, 0, sizeof(S));
+	S.state = (uint32_t *)scr;
+	S.flist_p = S.state + 2u * num_ctx;
+	S.flist_s = S.flist_p + num_ctx;
+	S.seqs = scr + words * 4u;
+	S.draws = S.seqs + tb;
+	S.kind = S.draws + tb;
+	S.fb = S.kind + tb;
+	S.num_ctx = num_ctx;
+	S.fpc = fpc;
+	S.packed = 2u * n;
+	S.iters = P->secondary_iterations;
+	S.model_needed = mneed;
+	S.raw_size = raw_frame_size(&ctx[0], n);
+	S.fb_eligible = cap1 == S.raw_size && P->uncompressed_fallback_enabled;
+	S.err_floor = ERRV(MAX_CODE);
+	S.err_small = ERRV(DST_TOO_SMALL);
+	S.err_mismatch = ERRV(SRC_SIZE_MISMATCH);
+	S.err_too_large = ERRV(HDR_CMP_SIZE_TOO_LARGE);
+	S.status = b->sizes;
+	S.src = b->src;
+	S.src_stride = b->src_stride;
+	S.sample_bytes = bytes;
+	S.n = n;
+	S.dst = b->dst;
+	S.dst_stride = b->dst_stride;
+	S.checksum = P->checksum_enabled ? 1u : 0u;
+	for (c = 0; c < num_ctx; c++) {
+		host_state[2u * c] = ctx[c].sequence_number;
+		host_state[2u * c + 1u] = ctx[c].model_size;
+	}
+	e = airs_dev_h2d(dev, S.state, host_state, 8u * (size_t)num_ctx);
+	if (!is_err(e))
+		e = airs_dev_memset(dev, S.fb, 0, tb);
+	/* work buffers: strided, or a pointer per context */
+	if (!is_err(e) && mneed) {
+		uint64_t base = (uint64_t)(uintptr_t)ctx[0].work_buf;
+		int ok = 1, al = 1;
+
+		mstride = num_ctx > 1 ? (uint64_t)(uintptr_t)ctx[1].work_buf - base : 0;
+		for (c = 0; c < num_ctx; c++) {
+			ok = ok && (uint64_t)(uintptr_t)ctx[c].work_buf == base + c * mstride;
+			al = al && ((uintptr_t)ctx[c].work_buf & 15u) == 0;
+		}
+		if (ok) {
+			mbase = ctx[0].work_buf;
+			S.model = mbase;
+			S.model_stride = mstride;
+		} else {
+			uint64_t *hp = calloc(num_ctx, sizeof(uint64_t));
+
+			d_ptr = airs_dev_scratch(dev, SLOT_AUX, (size_t)num_ctx * 8u);
+			if (!hp || !d_ptr) {
+				free(hp);
+				e = ERRV(GENERIC);
+			} else {
+				for (c = 0; c < num_ctx; c++)
+					hp[c] = (uint64_t)(uintptr_t)ctx[c].work_buf;
+				e = airs_dev_h2d(dev, d_ptr, hp, (size_t)num_ctx * 8u);
+				if (!is_err(e))
+					e = airs_dev_sync(dev);
+				free(hp);
+				S.model_ptrs = d_ptr;
+			}
+		}
+		(void)al;
+	}
+	if (!is_err(e) && P->checksum_enabled) {
+		d_ck = airs_dev_scratch(dev, SLOT_CK, (size_t)total * 4u);
+		e = d_ck ? airs_dev_checksum(dev, b->src, b->src_stride, bytes, n, total, NULL, d_ck) : ERRV(GENERIC);
+		S.checksums = d_ck;
+	}
+	if (!is_err(e) && (b->flags & CMP_GPU_AUTO_RICE)) {
+		d_g = airs_dev_scratch(dev, SLOT_G, (size_t)total * 4u);
+		if (!d_g)
+			e = ERRV(GENERIC);
+	}
+	for (a = 0; a <= fpc && !is_err(e); a++) {
+		S.prev = (int32_t)a - 1;
+		S.cur = a < fpc ? (int32_t)a : -1;
+		e = airs_dev_fb_step(dev, &S);
+		if (!is_err(e) && a > 0 && S.fb_eligible)
+			e = airs_dev_fb_copy(dev, &S);
+		if (a == fpc)
+			break;
+		for (uint32_t which = 0; which < (S.iters ? 2u : 1u) && !is_err(e); which++) {
+			const struct pass *Q = which ? ps : pp;
+			struct airs_launch L;
+
+			memset(&L, 0, sizeof(L));
+			L.src = b->src;
+			L.src_stride = b->src_stride;
+			L.sample_bytes = bytes;
+			L.is_unsigned = b->type == CMP_GPU_U16;
+			L.n = n;
+			L.num_frames = num_ctx;
+			L.frame_list = which ? S.flist_s : S.flist_p;
+			L.dst = b->dst;
+			L.dst_stride = b->dst_stride;
+			L.cap = (uint64_t)cap1 < frame_worst(n) ? cap1 : (uint32_t)frame_worst(n);
+			L.preprocessing = Q->pre;
+			L.encoder_type = Q->enc;
+			L.encoder_param = Q->par;
+			L.outlier_param = Q->outlier_param;
+			if (d_g && Q->enc == CMP_ENCODER_GOLOMB_ZERO) {
+				L.auto_rice = 1;
+				L.frame_g_scratch = d_g;
+				L.frame_g_frames = total;
+			}
+			L.model_mode = mneed ? (which ? AIRS_MODEL_UPDATE : AIRS_MODEL_STORE) : AIRS_MODEL_NONE;
+			L.model_rate = P->model_rate;
+			L.model = mbase;
+			L.model_stride = mstride;
+			L.model_div = fpc;
+			L.model_ptrs = d_ptr;
+			L.model_ptrs_al16 = 0;
+			L.fail_bit = model_fail_bit(cap1, n);
+			L.seqs = S.seqs;
+			L.checksum_enabled = S.checksum;
+			L.checksums = d_ck;
+			L.status = b->sizes;
+			e = airs_dev_encode(dev, &L);
+		}
+	}
+	/* the one read-back: identifier draws and the final context states */
+	if (!is_err(e))
+		e = airs_dev_d2h(dev, host_draws, S.draws, total);
+	if (!is_err(e))
+		e = airs_dev_d2h(dev, host_state, S.state, 8u * (size_t)num_ctx);
+	if (!is_err(e))
+		e = airs_dev_sync(dev);
+	if (is_err(e))
+		goto out;
+	for (c = 0; c < num_ctx; c++) {
+		uint64_t id = ctx[c].identifier;
+
+		for (a = 0; a < fpc; a++) {
+			const uint32_t f = c * fpc + a;
+
+			for (uint32_t k = 0; k < host_draws[f]; k++)
+				id = next_identifier();
+			ids[f] = id;
+		}
+		ctx[c].identifier = id;
+		ctx[c].sequence_number = (uint8_t)host_state[2u * c];
+		ctx[c].model_size = host_state[2u * c + 1u];
+	}
+	{
+		uint64_t *d_ids = airs_dev_scratch(dev, SLOT_IDS, (size_t)total * 8u);
+
+		if (!d_ids || is_err(airs_dev_h2d(dev, d_ids, ids, (size_t)total * 8u)))
+			e = ERRV(GENERIC);
+		else
+			e = airs_dev_patch_ids(dev, b->dst, b->dst_stride, total, 0, 1, d_ids, b->sizes);
+		if (!is_err(e))
+			e = airs_dev_sync(dev);
+	}
+out:
+	free(host_state);
+	free(host_draws);
+	return e;
+}
+
 uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx,
 			  uint32_t fpc, const struct cmp_gpu_batch *b)
 {
@@ -1138,7 +1401,13 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		free(draws);
 	}
 	if (exact) {
-		e = batch_exact(eng, ctx, num_ctx, fpc, b, plan, ids, ptrs);
+		struct pass pp, ps;
+
+		memset(&ps, 0, sizeof(ps));
+		if (!host_exact_forced() && device_exact_ok(ctx, num_ctx, b, n, &pp, &ps))
+			e = batch_device_exact(eng, ctx, num_ctx, fpc, b, &pp, &ps, ids);
+		else
+			e = batch_exact(eng, ctx, num_ctx, fpc, b, plan, ids, ptrs);
 		goto out;
 	}
 

@@ -70,7 +70,12 @@ struct KArgs {
 	// fused per-frame Rice selection (encode_kernel<..., AUTO>): per segment 16
 	// granules, epoch << 32 | sum over its samples of min((m+1) >> k, 16), k = 0..15
 	uint64_t *ktot;
+	// per batch frame header sequence numbers (device-planned launches), else seq
+	const uint8_t *seqs;
 };
+
+// frame_list entry of a launch position without a frame this launch
+#define AIRS_NO_FRAME 0xFFFFFFFFu
 
 // fused Rice selection: frames of at most AUTO_MAX_SPF segments (the frame's
 // 16 * spf candidate granules are read by one wave in AUTO_MAX_SPF / 4 loads

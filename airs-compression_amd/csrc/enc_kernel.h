@@ -138,6 +138,11 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 	const uint32_t gseg = lf * a.segs_per_frame + sif; // granule slot: frame-major
 	const uint32_t frame =
 		__builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
+	// a hole in a device-planned launch list (batch fallback path: the
+	// context takes the other pass this step, or none): the whole frame is
+	// skipped, and no segment of another frame waits on it
+	if (frame == AIRS_NO_FRAME)
+		return;
 	const bool is_first = sif == 0u;
 	const bool is_last = sif + 1u == a.segs_per_frame;
 	const uint32_t n = a.n;
@@ -1036,7 +1041,7 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 		}
 		const uint64_t id = a.ids ? a.ids[lf] : a.id_base + (uint64_t)lf * a.id_step;
 		uint32_t h[5];
-		header_words(h, size, 2u * n, id, a.seq, PRE, a.checksum ? 1u : 0u, ENC,
+		header_words(h, size, 2u * n, id, a.seqs ? a.seqs[frame] : a.seq, PRE, a.checksum ? 1u : 0u, ENC,
 			     PRE == PRE_MODEL ? a.model_rate : 0u, ENC == ENC_RAW ? 0u : gpar,
 			     ENC == ENC_RAW ? 0u : cd.outlier);
 		const uint32_t hwords = EXT_HDR ? 5u : 4u;

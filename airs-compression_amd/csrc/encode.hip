@@ -585,6 +585,136 @@ __global__ __launch_bounds__(256) void select_rice_kernel(const uint8_t *src, ui
 	}
 }
 
+// ---------------------------------------------------------------------
+// Batch fallback path on the device (cmp_gpu_compress, contexts with the
+// uncompressed fallback or frames that can fail): the context state machine
+// of compress_engine / cmp_compress_generic (reference cmp.c:228-246,
+// 342-393) runs here, one thread per context, so that a batch needs no host
+// round trip per acquisition step.  Per step a: fb_step_kernel resolves step
+// a-1 (outcome -> sequence number, fallback decision, identifier draws) and
+// plans step a (primary or secondary pass -> the launch lists of the two
+// encode launches); fb_copy_kernel writes the raw NONE + UNCOMPRESSED frames
+// of step a-1's fallbacks (and their model store).
+// ---------------------------------------------------------------------
+__global__ void fb_step_kernel(airs_fb_step a)
+{
+	const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+	if (c >= a.num_ctx)
+		return;
+	uint32_t seq = a.state[2u * c], msize = a.state[2u * c + 1u];
+	if (a.prev >= 0) {
+		const uint32_t f = c * a.fpc + (uint32_t)a.prev;
+		uint8_t fb = 0;
+		if (a.kind[f]) {
+			const uint32_t v = a.status[f];
+			if (v <= a.err_floor) {
+				seq++; // compress_engine succeeded (cmp.c:336)
+			} else if (a.fb_eligible && v == a.err_small) {
+				// cmp.c:375-392: reset (a draw), then the frame again as a
+				// primary NONE + UNCOMPRESSED pass (its own reset: a draw)
+				fb = 1;
+				a.draws[f] = (uint8_t)(a.draws[f] + 2u);
+				msize = a.packed;
+				if (a.raw_size > 0xFFFFFFu) {
+					a.status[f] = a.err_too_large; // header.c: size field
+					seq = 0;
+				} else {
+					a.status[f] = a.raw_size;
+					seq = 1;
+				}
+			}
+			// any other error: the sequence number stays (cmp.c returns early)
+		}
+		a.fb[f] = fb;
+	}
+	if (a.cur >= 0) {
+		const uint32_t f = c * a.fpc + (uint32_t)a.cur;
+		uint32_t lp = AIRS_NO_FRAME, ls = AIRS_NO_FRAME;
+		uint8_t kind = 0, draws = 0;
+		if (seq == 0 || seq > a.iters) { // cmp.c:228-237: reset, primary pass
+			seq = 0;
+			msize = a.packed;
+			draws = 1;
+			kind = 1;
+			lp = f;
+		} else if (a.model_needed && msize != a.packed) { // cmp.c:244-245
+			a.status[f] = a.err_mismatch;
+		} else {
+			kind = 2;
+			ls = f;
+		}
+		a.flist_p[c] = lp;
+		a.flist_s[c] = ls;
+		a.seqs[f] = (uint8_t)seq;
+		a.kind[f] = kind;
+		a.draws[f] = draws;
+	}
+	a.state[2u * c] = seq;
+	a.state[2u * c + 1u] = msize;
+}
+
+// raw frames of step `prev`'s fallbacks: header (16 B), the samples as
+// big-endian 16-bit words, the checksum; the model takes the samples (the
+// fallback is a primary pass: cmp.c:304-306).  Block (c, j) covers samples
+// [j * 2048, (j + 1) * 2048) of context c's frame.
+template <int W>
+__global__ __launch_bounds__(256) void fb_copy_kernel(airs_fb_step a)
+{
+	const uint32_t c = blockIdx.x, f = c * a.fpc + (uint32_t)a.prev;
+	if (!a.fb[f])
+		return;
+	const uint32_t n = a.n, i0 = blockIdx.y * 2048u + threadIdx.x * 8u;
+	const uint8_t *fs = (const uint8_t *)a.src + (uint64_t)f * a.src_stride;
+	uint8_t *fd = (uint8_t *)a.dst + (uint64_t)f * a.dst_stride;
+	uint16_t *fm = nullptr;
+	if (a.model_needed)
+		fm = (uint16_t *)(a.model_ptrs ? (uint8_t *)(uintptr_t)a.model_ptrs[c]
+					       : (uint8_t *)a.model + (uint64_t)c * a.model_stride);
+	uint32_t x[8];
+#pragma unroll
+	for (uint32_t q = 0; q < 8u; q++) {
+		const uint32_t i = i0 + q;
+		x[q] = i < n ? (W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fs)[i]
+				       : reinterpret_cast<const uint32_t *>(fs)[i] & 0xFFFFu)
+			     : 0u;
+	}
+	if (i0 + 8u <= n) { // 16 bytes at 16 + 2 i0: 16-byte aligned (dst is 8-byte, i0 a multiple of 8)
+		uint4 o;
+		o.x = __builtin_bswap32(x[0] << 16 | x[1]);
+		o.y = __builtin_bswap32(x[2] << 16 | x[3]);
+		o.z = __builtin_bswap32(x[4] << 16 | x[5]);
+		o.w = __builtin_bswap32(x[6] << 16 | x[7]);
+		uint8_t *p = fd + 16u + 2u * i0;
+		if (((uintptr_t)p & 15u) == 0u) {
+			*reinterpret_cast<uint4 *>(p) = o;
+		} else {
+			reinterpret_cast<uint2 *>(p)[0] = make_uint2(o.x, o.y);
+			reinterpret_cast<uint2 *>(p)[1] = make_uint2(o.z, o.w);
+		}
+	} else {
+		for (uint32_t q = 0; q < 8u && i0 + q < n; q++) {
+			fd[16u + 2u * (i0 + q)] = (uint8_t)(x[q] >> 8);
+			fd[17u + 2u * (i0 + q)] = (uint8_t)x[q];
+		}
+	}
+	if (fm) {
+		for (uint32_t q = 0; q < 8u && i0 + q < n; q++)
+			fm[i0 + q] = (uint16_t)x[q];
+	}
+	if (blockIdx.y == 0 && threadIdx.x == 0) {
+		uint32_t h[5];
+		header_words(h, a.raw_size, 2u * n, 0u, 0u, PRE_NONE, a.checksum ? 1u : 0u, ENC_RAW, 0u, 0u, 0u);
+#pragma unroll
+		for (uint32_t w = 0; w < 4u; w++)
+			reinterpret_cast<uint32_t *>(fd)[w] = __builtin_bswap32(h[w]);
+		if (a.checksum) {
+			const uint32_t ck = a.checksums[f];
+			for (uint32_t b = 0; b < 4u; b++)
+				fd[16u + 2u * n + b] = (uint8_t)(ck >> (24u - 8u * b));
+		}
+	}
+}
+
 // identifier patch after fallback resolution (header bytes 8..13)
 __global__ void patch_ids_kernel(uint8_t *dst, uint64_t stride, uint32_t num, uint32_t fadd, uint32_t fmul,
 				 const uint64_t *ids, const uint32_t *status)
@@ -1038,6 +1168,7 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	k.frame_list = L->frame_list;
 	k.frame_g = frame_g;
 	k.ktot = auto_fused ? e->ktot : nullptr;
+	k.seqs = L->seqs;
 	k.checksums = L->checksums;
 	k.ids = L->ids;
 	k.status = L->status;
@@ -1203,6 +1334,28 @@ extern "C" uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *
 			hipLaunchKernelGGL((select_rice_kernel<4, PRE_NONE>), dim3(num_frames), dim3(256), 0,
 					   e->stream, s, src_stride, n, out_g);
 	}
+	HIPCHECK(hipGetLastError());
+	return 0;
+}
+
+extern "C" uint32_t airs_dev_fb_step(struct airs_dev_engine *e, const struct airs_fb_step *s)
+{
+	if (!e || !s || !s->num_ctx)
+		return ERRV(E_GENERIC);
+	hipLaunchKernelGGL(fb_step_kernel, dim3((s->num_ctx + 255u) / 256u), dim3(256), 0, e->stream, *s);
+	HIPCHECK(hipGetLastError());
+	return 0;
+}
+
+extern "C" uint32_t airs_dev_fb_copy(struct airs_dev_engine *e, const struct airs_fb_step *s)
+{
+	if (!e || !s || !s->num_ctx || s->prev < 0 || !s->n)
+		return ERRV(E_GENERIC);
+	const dim3 grid(s->num_ctx, (s->n + 2047u) / 2048u);
+	if (s->sample_bytes == 2)
+		hipLaunchKernelGGL(fb_copy_kernel<2>, grid, dim3(256), 0, e->stream, *s);
+	else
+		hipLaunchKernelGGL(fb_copy_kernel<4>, grid, dim3(256), 0, e->stream, *s);
 	HIPCHECK(hipGetLastError());
 	return 0;
 }

@@ -434,7 +434,7 @@ def main():
     if key and key in gold:
         want = gold[key][rank]
     elif wl["layout"] == "block" and rank == 0:
-        want = gold["digest"]
+        want = gold["sha256"] if wl.get("stream") else gold["digest"]
     else:
         want = None
     bitexact = None

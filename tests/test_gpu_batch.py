@@ -22,6 +22,18 @@ def eng(prod):
     e.close()
 
 
+@pytest.fixture(params=["device", "host"])
+def exact_mode(request, monkeypatch):
+    """Batches that can fall back or fail run the context state machine on
+    the GPU (batch_device_exact) unless AIRS_HOST_EXACT=1 selects the
+    host-stepped path (batch_exact); both must equal the call loop."""
+    if request.param == "host":
+        monkeypatch.setenv("AIRS_HOST_EXACT", "1")
+    else:
+        monkeypatch.delenv("AIRS_HOST_EXACT", raising=False)
+    return request.param
+
+
 def _compare(prod, eng, orc, trial):
     params, kind, n, nctx, fpc, cap, srcs = bs.make_case(api, trial)
     want = bs.run_batch_host(orc, api, params, kind, n, nctx, fpc, cap, srcs)
@@ -29,7 +41,7 @@ def _compare(prod, eng, orc, trial):
     return got == want, want
 
 
-def test_batch_vs_call_loop(prod, eng, orc):
+def test_batch_vs_call_loop(prod, eng, orc, exact_mode):
     bad, fallbacks, errors = [], 0, 0
     for trial in range(300):
         ok, want = _compare(prod, eng, orc, trial)
@@ -46,7 +58,7 @@ def test_batch_vs_call_loop(prod, eng, orc):
     assert errors > 50 and fallbacks > 50, (errors, fallbacks)
 
 
-def test_batch_fallback_identifiers(prod, eng, orc):
+def test_batch_fallback_identifiers(prod, eng, orc, exact_mode):
     """Noise frames that do not compress: every frame falls back; identifiers
     advance by three draws per primary fallback and two per secondary one."""
     import numpy as np
@@ -65,7 +77,7 @@ def test_batch_fallback_identifiers(prod, eng, orc):
         assert all(r == 16 + 2 * n + 4 for r, _ in want[0])
 
 
-def test_batch_size_field_overflow_vs_call_loop(prod, eng, orc):
+def test_batch_size_field_overflow_vs_call_loop(prod, eng, orc, exact_mode):
     """4 Mi-sample frames whose worst case exceeds the 24-bit compressed-size
     field: noise frames fail with HDR_CMP_SIZE_TOO_LARGE even though the
     capacity holds the worst case, and the reference then does not advance
@@ -86,6 +98,42 @@ def test_batch_size_field_overflow_vs_call_loop(prod, eng, orc):
     want = bs.run_batch_host(orc, api, params, "u16", n, nctx, fpc, cap, srcs)
     assert api.error_name(want[0][0][0]) == "HDR_CMP_SIZE_TOO_LARGE", want[0][0][0]
     got = bs.run_batch_gpu(prod, eng, api, params, "u16", n, nctx, fpc, cap, srcs)
+    assert got == want
+
+
+@pytest.mark.parametrize("kind", ["i16_in_i32", "u16"])
+def test_batch_model_fallback_cfg5_shape(prod, eng, orc, exact_mode, kind):
+    """BASELINE config 5's parameters (DIFF + ZERO g=16, then 15 MODEL + MULTI
+    passes g=8 o=107 rate 11) with the uncompressed fallback and checksums on:
+    noise frames at scattered acquisition steps fall back (primary and
+    secondary), so contexts drift apart in their pass sequence.  Frames,
+    sizes, context states and work buffers equal the oracle's call loop."""
+    import numpy as np
+    P = api.CmpParams
+    params = P(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16,
+               secondary_iterations=15, secondary_preprocessing=3, secondary_encoder_type=2,
+               secondary_encoder_param=8, secondary_encoder_outlier=107, model_rate=11,
+               checksum_enabled=1, uncompressed_fallback_enabled=1)
+    rng = np.random.default_rng(55)
+    n, nctx, fpc = 8192 + 77, 12, 16
+    srcs = []
+    for c in range(nctx):
+        base = np.cumsum(rng.integers(-3, 4, n))
+        for a in range(fpc):
+            if rng.random() < 0.15:
+                v = rng.integers(-32768, 32768, n)  # noise: the frame falls back
+            else:
+                v = base + rng.integers(-4, 5, n)
+            v = v.astype(np.int64)
+            if kind == "u16":
+                srcs.append((v & 0xFFFF).astype(np.uint16))
+            else:
+                srcs.append(((v & 0xFFFF) | (rng.integers(-5, 5, n) << 16)).astype(np.int32))
+    cap = 26 + 6 * n
+    want = bs.run_batch_host(orc, api, params, kind, n, nctx, fpc, cap, srcs)
+    nfb = sum(1 for r, b in want[0] if b is not None and api.parse_header(b)["encoder_type"] == 0)
+    assert nfb > 10, nfb
+    got = bs.run_batch_gpu(prod, eng, api, params, kind, n, nctx, fpc, cap, srcs)
     assert got == want
 
 
