@@ -107,6 +107,9 @@ class AirsLib(CmpLib):
         L.cmp_gpu_encode_stream.argtypes = [c_void_p, c_uint32, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32,
                                             c_uint32, c_void_p, c_uint32, c_void_p]
         L.cmp_gpu_encode_stream.restype = c_uint32
+        L.cmp_gpu_pack_frames.argtypes = [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_uint32, c_void_p,
+                                          c_void_p]
+        L.cmp_gpu_pack_frames.restype = c_uint32
 
     def gpu_available(self) -> bool:
         return bool(self.lib.cmp_gpu_available())
@@ -163,6 +166,12 @@ class GpuEngine:
         return self.lib.lib.cmp_gpu_encode_stream(self.handle, KIND_TO_GPU[kind], src_ptr, num_samples,
                                                   preprocessing, encoder_type, encoder_param, encoder_outlier,
                                                   dst_ptr, dst_capacity, size_ptr)
+
+    def pack_frames(self, frames_ptr: int, frame_stride: int, frame_capacity: int, sizes_ptr: int,
+                    num_frames: int, out_ptr: int, offsets_ptr: int) -> int:
+        """cmp_gpu_pack_frames: strided frames -> back to back at 8-byte aligned offsets (device)."""
+        return self.lib.lib.cmp_gpu_pack_frames(self.handle, frames_ptr, frame_stride, frame_capacity, sizes_ptr,
+                                                num_frames, out_ptr, offsets_ptr)
 
     def synchronize(self) -> int:
         return self.lib.lib.cmp_gpu_synchronize(self.handle)

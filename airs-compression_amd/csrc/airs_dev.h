@@ -133,6 +133,13 @@ struct airs_fb_step {
 uint32_t airs_dev_fb_step(struct airs_dev_engine *e, const struct airs_fb_step *s);
 uint32_t airs_dev_fb_copy(struct airs_dev_engine *e, const struct airs_fb_step *s);
 
+/* frames f < num_frames of a strided buffer packed back to back at 8-byte
+ * aligned offsets (offsets[f], offsets[num_frames] = total; frames whose size
+ * is an error value take no bytes); reads only the compressed bytes */
+uint32_t airs_dev_pack_frames(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
+			      uint32_t max_frame_bytes, const uint32_t *sizes, uint32_t num_frames,
+			      uint32_t err_floor, void *out, uint64_t *offsets);
+
 /* XXH32 (seed 419764627) over each frame's samples as big-endian 16-bit words */
 uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
 			   uint32_t sample_bytes, uint32_t n, uint32_t num_frames,

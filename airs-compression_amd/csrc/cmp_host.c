@@ -656,6 +656,19 @@ uint32_t cmp_gpu_encode_stream(struct cmp_gpu_engine *engine, enum cmp_gpu_sampl
 				      dst, dst_capacity, size);
 }
 
+uint32_t cmp_gpu_pack_frames(struct cmp_gpu_engine *engine, const void *frames, uint64_t frame_stride,
+			     uint32_t frame_capacity, const uint32_t *sizes, uint32_t num_frames, void *out,
+			     uint64_t *offsets)
+{
+	if (!engine || !frames || !sizes || !out || !offsets || !num_frames)
+		return ERRV(GENERIC);
+	if ((frame_stride & 7u) || ((uintptr_t)frames & 7u) || ((uintptr_t)out & 7u) ||
+	    (num_frames > 1 && frame_stride < frame_capacity))
+		return ERRV(DST_UNALIGNED);
+	return airs_dev_pack_frames(engine->dev, frames, frame_stride, frame_capacity, sizes, num_frames,
+				    ERRV(MAX_CODE), out, offsets);
+}
+
 uint32_t cmp_gpu_synthesize(struct cmp_gpu_engine *engine, void *dst, uint32_t sample_bytes, uint64_t seed,
 			    uint32_t frame0, uint32_t samples_per_frame, uint32_t num_frames, uint64_t stride,
 			    uint32_t noise_w)

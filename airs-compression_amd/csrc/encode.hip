@@ -715,6 +715,60 @@ __global__ __launch_bounds__(256) void fb_copy_kernel(airs_fb_step a)
 	}
 }
 
+// ---------------------------------------------------------------------
+// Frame packing for the multi-GPU gather (cmp_gpu_pack_frames, shard.py):
+// the frames of a strided batch buffer, back to back at 8-byte aligned
+// offsets, reading only the compressed bytes (rounded up to 8).
+// ---------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void pack_scan_kernel(const uint32_t *sizes, uint32_t num, uint32_t err_floor,
+							 uint64_t *offsets)
+{
+	__shared__ uint64_t s_w[16];
+	__shared__ uint64_t s_carry;
+	const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+	if (t == 0)
+		s_carry = 0;
+	__syncthreads();
+	for (uint32_t base = 0; base < num; base += 1024u) {
+		const uint32_t i = base + t;
+		const uint32_t sz = i < num ? sizes[i] : 0u;
+		const uint64_t v = (sz > err_floor) ? 0u : ((uint64_t)sz + 7u) & ~7ull;
+		uint64_t inc = v;
+#pragma unroll
+		for (uint32_t d = 1; d < 64u; d <<= 1) {
+			const uint64_t o = __shfl_up(inc, d, 64);
+			inc += lane >= d ? o : 0u;
+		}
+		if (lane == 63u)
+			s_w[w] = inc;
+		__syncthreads();
+		uint64_t pre = s_carry;
+		for (uint32_t k = 0; k < w; k++)
+			pre += s_w[k];
+		if (i < num)
+			offsets[i] = pre + inc - v;
+		__syncthreads();
+		if (t == 1023u)
+			s_carry = pre + inc;
+		__syncthreads();
+	}
+	if (t == 0)
+		offsets[num] = s_carry;
+}
+
+__global__ __launch_bounds__(256) void pack_copy_kernel(const uint8_t *src, uint64_t stride, const uint32_t *sizes,
+							uint32_t err_floor, const uint64_t *offsets, uint8_t *out)
+{
+	const uint32_t f = blockIdx.x, sz = sizes[f];
+	if (sz > err_floor)
+		return;
+	const uint32_t nw = (sz + 7u) >> 3; // 8-byte words of the frame
+	const uint2 *s8 = reinterpret_cast<const uint2 *>(src + (uint64_t)f * stride);
+	uint2 *o8 = reinterpret_cast<uint2 *>(out + offsets[f]);
+	for (uint32_t j = blockIdx.y * 1024u + threadIdx.x; j < nw && j < (blockIdx.y + 1u) * 1024u; j += 256u)
+		o8[j] = s8[j];
+}
+
 // identifier patch after fallback resolution (header bytes 8..13)
 __global__ void patch_ids_kernel(uint8_t *dst, uint64_t stride, uint32_t num, uint32_t fadd, uint32_t fmul,
 				 const uint64_t *ids, const uint32_t *status)
@@ -1356,6 +1410,21 @@ extern "C" uint32_t airs_dev_fb_copy(struct airs_dev_engine *e, const struct air
 		hipLaunchKernelGGL(fb_copy_kernel<2>, grid, dim3(256), 0, e->stream, *s);
 	else
 		hipLaunchKernelGGL(fb_copy_kernel<4>, grid, dim3(256), 0, e->stream, *s);
+	HIPCHECK(hipGetLastError());
+	return 0;
+}
+
+extern "C" uint32_t airs_dev_pack_frames(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
+					uint32_t max_frame_bytes, const uint32_t *sizes, uint32_t num_frames,
+					uint32_t err_floor, void *out, uint64_t *offsets)
+{
+	if (!e || !src || !sizes || !out || !offsets || !num_frames || (src_stride & 7u) || ((uintptr_t)src & 7u) ||
+	    ((uintptr_t)out & 7u))
+		return ERRV(E_GENERIC);
+	hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(1024), 0, e->stream, sizes, num_frames, err_floor, offsets);
+	const uint32_t ny = (((uint64_t)max_frame_bytes + 7u) / 8u + 1023u) / 1024u;
+	hipLaunchKernelGGL(pack_copy_kernel, dim3(num_frames, ny ? ny : 1u), dim3(256), 0, e->stream,
+			   (const uint8_t *)src, src_stride, sizes, err_floor, offsets, (uint8_t *)out);
 	HIPCHECK(hipGetLastError());
 	return 0;
 }

@@ -88,6 +88,11 @@ WORKLOADS = {
                              secondary_encoder_type=MULTI, secondary_encoder_param=8,
                              secondary_encoder_outlier=107, model_rate=11)),
 }
+# configs[4] with the uncompressed fallback enabled: every frame may fall back,
+# so the batch runs the context state machine on the device (the frames are
+# those of cfg5: this data always compresses)
+WORKLOADS["cfg5fb"] = dict(WORKLOADS["cfg5"], desc=WORKLOADS["cfg5"]["desc"] + ", uncompressed fallback enabled",
+                           params=dict(WORKLOADS["cfg5"]["params"], uncompressed_fallback_enabled=1))
 
 
 def sample_bytes(wl):
@@ -469,7 +474,9 @@ def main():
     if world > 1 and not args.no_gather:
         bs = sets[0]
         gather, g = pkg.shard.gather_frames_timed(dist, bs.dst, bs.dstride, bs.sizes, nf, rank, world,
-                                                  layout="roundrobin", patch_base=0)
+                                                  layout="roundrobin", patch_base=0,
+                                                  params=api.CmpParams(**wl["params"]), engine=eng,
+                                                  frame_capacity=bs.cap)
         if g is not None:
             host_all = g.data.cpu().numpy()
             offs, lens = g.offsets.numpy(), g.sizes.numpy()
@@ -502,6 +509,8 @@ def main():
         "cfg4": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL>: one launch per step",
         "cfg5": "encode_kernel<4,DIFF,ZERO,Rice,STORE> + 15 x encode_kernel<4,MODEL,MULTI,Rice,UPDATE>: 16 "
                 "launches per step (one per acquisition)",
+        "cfg5fb": "per acquisition: fb_step_kernel + fb_copy_kernel + encode_kernel<4,DIFF,ZERO,Rice,STORE> + "
+                  "encode_kernel<4,MODEL,MULTI,Rice,UPDATE> (frame-list holes)",
     }
     result = None
     if rank == 0:

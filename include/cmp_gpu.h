@@ -130,6 +130,20 @@ uint32_t cmp_gpu_encode_stream(struct cmp_gpu_engine *engine, enum cmp_gpu_sampl
 			       enum cmp_encoder_type encoder_type, uint32_t encoder_param, uint32_t encoder_outlier,
 			       void *dst, uint32_t dst_capacity, uint32_t *size);
 
+/*
+ * Pack the frames of a strided batch output (frame f at frames + f*frame_stride,
+ * sizes[f] bytes, as cmp_gpu_compress leaves them) back to back into out: frame
+ * f at out + offsets[f], offsets 8-byte aligned, offsets[num_frames] = the
+ * total.  Frames whose size is an error value take no bytes.  Reads only the
+ * compressed bytes (rounded up to 8).  All pointers are device pointers;
+ * out must hold the sum of the sizes rounded up to 8 each (at most
+ * num_frames * frame_capacity rounded up to 8).  Asynchronous.  This is the
+ * compaction step of the multi-GPU gather (shard.py); build-defined extension.
+ */
+uint32_t cmp_gpu_pack_frames(struct cmp_gpu_engine *engine, const void *frames, uint64_t frame_stride,
+			     uint32_t frame_capacity, const uint32_t *sizes, uint32_t num_frames, void *out,
+			     uint64_t *offsets);
+
 /* wait for all work queued on the engine */
 uint32_t cmp_gpu_synchronize(struct cmp_gpu_engine *engine);
 

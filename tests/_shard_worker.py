@@ -62,13 +62,26 @@ def run(rank, world, port, nf, n, layout, mode):
             else:
                 raise AssertionError("error value was not reported")
             return
+        if mode == "patch_refused":
+            try:
+                shard.gather_frames_timed(dist, dst_t, stride, sizes_t, nf, rank, world, layout=layout,
+                                          patch_base=0, params=api.CmpParams(**PARAMS, secondary_iterations=2))
+            except ValueError as e:
+                assert "identifier patching" in str(e)
+            else:
+                raise AssertionError("patching frames with secondary passes was not refused")
+            return
         stats, g = shard.gather_frames_timed(dist, dst_t, stride, sizes_t, nf, rank, world, layout=layout,
-                                             patch_base=1000)
+                                             patch_base=1000, params=api.CmpParams(**PARAMS))
         if rank != 0:
             assert g is None and stats is None
             return
         assert g.num_frames == nf * world
         assert stats["frames"] == nf * world and stats["bytes_total"] == int(g.data.numel())
+        # the packing read only the compressed bytes (rounded up to 8 per frame)
+        own = sizes_t[:nf].to(torch.int64)
+        assert stats["root_pack_bytes_read"] == int(((own + 7) // 8 * 8).sum())
+        assert stats["root_pack_bytes_read"] < int(own.sum()) + 8 * nf
         want_dst, wstride, want_sizes = encode(orc, orc_ext, api, list(range(nf * world)), n, seed)
         stream = g.ordered().numpy()
         pos = 0

@@ -134,6 +134,22 @@ uint32_t airs_dev_encode_stream(struct airs_dev_engine *e, const void *src, uint
 	return 0;
 }
 
+uint32_t airs_dev_pack_frames(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
+			      uint32_t max_frame_bytes, const uint32_t *sizes, uint32_t num_frames,
+			      uint32_t err_floor, void *out, uint64_t *offsets)
+{
+	uint64_t o = 0;
+	(void)e, (void)max_frame_bytes;
+	for (uint32_t f = 0; f < num_frames; f++) {
+		const uint32_t sz = sizes[f] > err_floor ? 0u : sizes[f];
+		offsets[f] = o;
+		memcpy((uint8_t *)out + o, (const uint8_t *)src + (uint64_t)f * src_stride, sz);
+		o += ((uint64_t)sz + 7u) & ~7ull;
+	}
+	offsets[num_frames] = o;
+	return 0;
+}
+
 uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src, uint64_t src_stride, uint32_t sample_bytes,
 			   uint32_t n, uint32_t num_frames, const uint32_t *frame_list, uint32_t *out)
 {

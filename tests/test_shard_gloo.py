@@ -1,6 +1,8 @@
 """Multi-rank path of SURVEY.md 8(e) on CPU: the frame gather to rank 0
-(all_gather of sizes, compaction, point-to-point sends, f-order table,
-identifier patch), world size 2 over gloo."""
+(all_gather of sizes, packing at 8-byte aligned offsets that reads only the
+compressed bytes, batched point-to-point receives into the root buffer,
+f-order table, identifier patch and its refusal for parameter sets whose
+identifiers depend on the outcomes), world size 2 over gloo."""
 import socket
 
 import pytest
@@ -33,3 +35,7 @@ def test_gather_world2_ragged_small(orc):
 
 def test_gather_world2_error_value(orc):
     _spawn(3, 500, "roundrobin", "error")
+
+
+def test_gather_world2_patch_refused_with_secondary_passes(orc):
+    _spawn(3, 500, "roundrobin", "patch_refused")
