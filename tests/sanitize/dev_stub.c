@@ -81,6 +81,8 @@ uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L)
 		return ERRV(1u);
 	for (uint32_t j = 0; j < L->num_frames; j++) {
 		const uint32_t f = L->frame_list ? L->frame_list[j] : L->frame_add + j * L->frame_mul;
+		if (f == 0xFFFFFFFFu) /* AIRS_NO_FRAME: a hole in a device-planned list */
+			continue;
 		const uint64_t h = mix(e->salt++ ^ ((uint64_t)f << 32) ^ L->n);
 		/* every input byte the kernel would read is read here too */
 		const uint8_t *src = (const uint8_t *)L->src + (uint64_t)f * L->src_stride;
@@ -147,6 +149,88 @@ uint32_t airs_dev_pack_frames(struct airs_dev_engine *e, const void *src, uint64
 		o += ((uint64_t)sz + 7u) & ~7ull;
 	}
 	offsets[num_frames] = o;
+	return 0;
+}
+
+/* the per-context state machine of fb_step_kernel (encode.hip), on the host */
+uint32_t airs_dev_fb_step(struct airs_dev_engine *e, const struct airs_fb_step *a)
+{
+	if (!e || !a || !a->num_ctx)
+		return ERRV(1u);
+	for (uint32_t c = 0; c < a->num_ctx; c++) {
+		uint32_t seq = a->state[2u * c], msize = a->state[2u * c + 1u];
+		if (a->prev >= 0) {
+			const uint32_t f = c * a->fpc + (uint32_t)a->prev;
+			uint8_t fb = 0;
+			if (a->kind[f]) {
+				const uint32_t v = a->status[f];
+				if (v <= a->err_floor) {
+					seq++;
+				} else if (a->fb_eligible && v == a->err_small) {
+					fb = 1;
+					a->draws[f] = (uint8_t)(a->draws[f] + 2u);
+					msize = a->packed;
+					a->status[f] = a->raw_size > 0xFFFFFFu ? a->err_too_large : a->raw_size;
+					seq = a->raw_size > 0xFFFFFFu ? 0u : 1u;
+				}
+			}
+			a->fb[f] = fb;
+		}
+		if (a->cur >= 0) {
+			const uint32_t f = c * a->fpc + (uint32_t)a->cur;
+			uint32_t lp = 0xFFFFFFFFu, ls = 0xFFFFFFFFu;
+			uint8_t kind = 0, draws = 0;
+			if (seq == 0 || seq > a->iters) {
+				seq = 0;
+				msize = a->packed;
+				draws = 1;
+				kind = 1;
+				lp = f;
+			} else if (a->model_needed && msize != a->packed) {
+				a->status[f] = a->err_mismatch;
+			} else {
+				kind = 2;
+				ls = f;
+			}
+			a->flist_p[c] = lp;
+			a->flist_s[c] = ls;
+			a->seqs[f] = (uint8_t)seq;
+			a->kind[f] = kind;
+			a->draws[f] = draws;
+		}
+		a->state[2u * c] = seq;
+		a->state[2u * c + 1u] = msize;
+	}
+	return 0;
+}
+
+/* fb_copy_kernel: raw frames of the previous step's fallbacks */
+uint32_t airs_dev_fb_copy(struct airs_dev_engine *e, const struct airs_fb_step *a)
+{
+	if (!e || !a || !a->num_ctx || a->prev < 0 || !a->n)
+		return ERRV(1u);
+	for (uint32_t c = 0; c < a->num_ctx; c++) {
+		const uint32_t f = c * a->fpc + (uint32_t)a->prev;
+		if (!a->fb[f])
+			continue;
+		const uint8_t *fs = (const uint8_t *)a->src + (uint64_t)f * a->src_stride;
+		uint8_t *fd = (uint8_t *)a->dst + (uint64_t)f * a->dst_stride;
+		uint16_t *fm = NULL;
+		if (a->model_needed)
+			fm = (uint16_t *)(a->model_ptrs ? (uint8_t *)(uintptr_t)a->model_ptrs[c]
+							: (uint8_t *)a->model + (uint64_t)c * a->model_stride);
+		memset(fd, 0, 16);
+		for (uint32_t i = 0; i < a->n; i++) {
+			const uint16_t x = a->sample_bytes == 2 ? ((const uint16_t *)fs)[i]
+							       : (uint16_t)((const uint32_t *)fs)[i];
+			fd[16u + 2u * i] = (uint8_t)(x >> 8);
+			fd[17u + 2u * i] = (uint8_t)x;
+			if (fm)
+				fm[i] = x;
+		}
+		if (a->checksum)
+			memcpy(fd + 16u + 2u * a->n, &a->checksums[f], 4);
+	}
 	return 0;
 }
 
