@@ -4,7 +4,7 @@
 #   passes per workload -> traffic json.
 # usage: bash scripts/gpu_r02.sh TAG [workloads...]   (SKIP_TESTS=1 to skip pytest)
 TAG=${1:-r02}; shift
-WLS=${@:-cfg2 cfg3 cfg4 cfg5}
+WLS=${@:-cfg2 cfg2s cfg3 cfg4 cfg5 cfg5fb}
 O=gpurun_out/$TAG
 cd "$GRAFT_REPO_ROOT" && mkdir -p $O && export TMPDIR=/tmp || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
