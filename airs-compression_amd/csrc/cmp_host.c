@@ -704,6 +704,12 @@ static int affine_u64(const uint64_t *v, uint32_t cnt, uint64_t *step)
 	return 1;
 }
 
+/* size of the raw (fallback) frame of a context, as cmp_compress_generic (cmp.c:342-393) */
+static uint32_t raw_frame_size(const struct cmp_context *ctx, uint32_t n)
+{
+	return CMP_HDR_SIZE + 2u * n + (ctx->params.checksum_enabled ? CMP_CHECKSUM_SIZE : 0u);
+}
+
 /* Launch cnt frames that share one pass: launch frame j is batch frame
  * fl[j] (host list) or add + j*mul; output capacity cap. */
 static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t fpc,
@@ -830,18 +836,16 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 	L.outlier_param = P->outlier_param;
 	L.model_mode = P->model_mode;
 	L.model_rate = prm->model_rate;
-	L.fail_bit = model_fail_bit(cap, n);
+	/* a frame that runs out of room in a fallback-sized first attempt falls
+	 * back, and the fallback stores the whole model: no fail bit needed */
+	L.fail_bit = (prm->uncompressed_fallback_enabled && cap == raw_frame_size(&ctx[f0 / fpc], n))
+			     ? UINT64_MAX
+			     : model_fail_bit(cap, n);
 	L.seq = P->seq;
 	L.checksum_enabled = prm->checksum_enabled ? 1u : 0u;
 	L.checksums = d_ck;
 	L.status = b->sizes;
 	return airs_dev_encode(dev, &L);
-}
-
-/* size of the raw (fallback) frame of a context, as cmp_compress_generic (cmp.c:342-393) */
-static uint32_t raw_frame_size(const struct cmp_context *ctx, uint32_t n)
-{
-	return CMP_HDR_SIZE + 2u * n + (ctx->params.checksum_enabled ? CMP_CHECKSUM_SIZE : 0u);
 }
 
 /* launch every frame of `list` (batch frames of one acquisition step): one
@@ -1238,7 +1242,9 @@ static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_contex
 			L.model_div = fpc;
 			L.model_ptrs = d_ptr;
 			L.model_ptrs_al16 = 0;
-			L.fail_bit = model_fail_bit(cap1, n);
+			/* a first attempt that runs out of room falls back, and the
+			 * fallback stores the whole model: no fail bit needed then */
+			L.fail_bit = S.fb_eligible ? UINT64_MAX : model_fail_bit(cap1, n);
 			L.seqs = S.seqs;
 			L.checksum_enabled = S.checksum;
 			L.checksums = d_ck;

@@ -84,7 +84,11 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 	// 0 with a model, whose chunk-0 update needs the bit offset first.
 	// (AUTO: two images, so that four workgroups fit a CU with 32-bit images)
 	constexpr uint32_t NIMG = AUTOK ? 2u : seg_images(W, MODEL);
-	constexpr uint32_t LBC = (MODEL || CH < 2) ? 0u : NIMG - 1u;
+	// With a model the update of chunk 0 needs the bit offset only to find the
+	// samples the reference's loop never reached (fail_bit); FULL model
+	// launches are host-checked to have no fail bit, so their look-back
+	// overlaps the packing like the others
+	constexpr uint32_t LBC = ((MODEL && !FULL) || CH < 2) ? 0u : NIMG - 1u;
 	constexpr uint32_t RW = EPT * W / 16u; // uint4 per lane per chunk
 	constexpr uint32_t MRW = EPT / 8u;      // uint4 of 16-bit model values per lane per chunk
 	constexpr bool EXT_HDR = !(PRE == PRE_NONE && ENC == ENC_RAW);

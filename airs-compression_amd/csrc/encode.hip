@@ -1289,6 +1289,10 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	if (L->model_mode != AIRS_MODEL_NONE || L->preprocessing == PRE_IWT)
 		full = full && (L->model_ptrs ? L->model_ptrs_al16 != 0u
 					      : ((uintptr_t)L->model & 15u) == 0u && (L->model_stride & 15u) == 0u);
+	// FULL model launches run the look-back after the packing (enc_kernel.h
+	// LBC): only when no frame can stop early (no fail bit)
+	if (L->model_mode != AIRS_MODEL_NONE)
+		full = full && L->fail_bit == UINT64_MAX;
 	if (pipe) {
 		r = pipe_encode(k, L->sample_bytes, L->preprocessing, L->encoder_type, rice, e->stream);
 		if (r)
