@@ -939,7 +939,7 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 							if (DBG(256u))
 								atomicAdd(a.ticket + 23, 1u);
 						}
-						if ((DBG(65536u)) && a.dbgts)
+						if ((DBG(65536u)) && a.dbgts && !AUTOK)
 							a.dbgts[8u * gseg + 6u] = spins;
 						pred = (uint32_t)tv;
 					}

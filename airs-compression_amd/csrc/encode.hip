@@ -512,6 +512,193 @@ __global__ __launch_bounds__(64) void checksum_kernel(const uint8_t *src, uint64
 	out[frame] = h;
 }
 
+// one XXH32 round with the input's P2 product already formed: add, rotate,
+// multiply as three dependent instructions (the compiler would fuse the add
+// into a 64-bit v_mad_u64_u32, whose latency is longer)
+__device__ __forceinline__ uint32_t xxh_round_pre(uint32_t acc, uint32_t yp2)
+{
+	asm volatile("v_add_u32 %0, %0, %1\n\tv_alignbit_b32 %0, %0, %0, 19\n\tv_mul_lo_u32 %0, %0, %2"
+		     : "+v"(acc)
+		     : "v"(yp2), "s"(XP1));
+	return acc;
+}
+
+// XXH32 with the accumulator chains split from their inputs: one consumer
+// wave runs the 64 serial chains of 16 frames (4 lanes per frame, as
+// checksum_kernel) and does only add, rotate, multiply per round; three
+// producer waves load the stripes, form the big-endian words and multiply
+// by P2 into a two-slot LDS ring, one slot ahead of the consumer.  A
+// round costs the chain wave 3 VALU instructions instead of 5 (two of
+// which were quarter-rate multiplies).  Frames of a block share n, so all
+// chains take the same number of rounds.
+#define CK_RS 256u // rounds per ring slot
+template <int W>
+__global__ __launch_bounds__(256) void checksum_pc_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
+							  uint32_t num_frames, const uint32_t *frame_list,
+							  uint32_t *out)
+{
+	// ring[slot][round / 4][chain] holds the inputs of rounds 4 rb .. 4 rb + 3
+	__shared__ uint4 ring[2][CK_RS / 4][64];
+	__shared__ uint64_t s_fbase[16];
+	const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+	const uint32_t nloc = min(16u, num_frames - blockIdx.x * 16u);
+	if (tid < 16u) {
+		const uint32_t lf = blockIdx.x * 16u + tid;
+		const uint32_t fr = tid < nloc ? (frame_list ? frame_list[lf] : lf) : 0u;
+		s_fbase[tid] = (uint64_t)(uintptr_t)(src + (uint64_t)fr * stride);
+	}
+	__syncthreads();
+	const uint32_t len = 2u * n;
+	const uint32_t stripes = len >= 16u ? n / 8u : 0u;
+	const uint32_t nslots = (stripes + CK_RS - 1u) / CK_RS;
+
+	// every load of a slot is issued before the first is used (22 stripes per
+	// producer thread in flight); unaligned frames take the per-sample path
+	constexpr uint32_t PER = (16u * CK_RS + 191u) / 192u;
+	constexpr uint32_t LPS = W == 2 ? 1u : 2u; // 16-byte loads per stripe
+#ifndef AIRS_CK_ABL // experiments: 1 producers idle, 2 consumer idle
+#define AIRS_CK_ABL 0
+#endif
+	auto produce = [&](uint32_t slot) {
+		if (AIRS_CK_ABL == 1)
+			return;
+		uint32_t *R = reinterpret_cast<uint32_t *>(&ring[slot & 1u][0][0]);
+		const uint32_t r0 = slot * CK_RS;
+		uint4 v[PER][LPS];
+#pragma unroll
+		for (uint32_t k = 0; k < PER; k++) {
+			const uint32_t it = tid - 64u + 192u * k;
+			const uint32_t fl = it / CK_RS, rr = it - fl * CK_RS, r = r0 + rr;
+			const uint8_t *f = reinterpret_cast<const uint8_t *>((uintptr_t)s_fbase[fl < 16u ? fl : 0u]);
+			if (it < 16u * CK_RS && fl < nloc && r < stripes && ((uintptr_t)f & 15u) == 0u) {
+				// from the kernel argument, so that the loads are global, not flat
+				const uint4 *g = reinterpret_cast<const uint4 *>(src + ((uintptr_t)f - (uintptr_t)src));
+#pragma unroll
+				for (uint32_t h = 0; h < LPS; h++)
+					v[k][h] = g[LPS * r + h];
+			}
+		}
+#pragma unroll
+		for (uint32_t k = 0; k < PER; k++) {
+			const uint32_t it = tid - 64u + 192u * k;
+			const uint32_t fl = it / CK_RS, rr = it - fl * CK_RS, r = r0 + rr;
+			if (it >= 16u * CK_RS || fl >= nloc || r >= stripes)
+				continue;
+			const uint8_t *f = reinterpret_cast<const uint8_t *>((uintptr_t)s_fbase[fl]);
+			uint32_t y[4];
+			if (((uintptr_t)f & 15u) == 0u) {
+				if (W == 2) {
+					y[0] = __builtin_amdgcn_perm(v[k][0].x, v[k][0].x, 0x02030001u);
+					y[1] = __builtin_amdgcn_perm(v[k][0].y, v[k][0].y, 0x02030001u);
+					y[2] = __builtin_amdgcn_perm(v[k][0].z, v[k][0].z, 0x02030001u);
+					y[3] = __builtin_amdgcn_perm(v[k][0].w, v[k][0].w, 0x02030001u);
+				} else {
+					y[0] = be_pair(v[k][0].x & 0xFFFFu, v[k][0].y & 0xFFFFu);
+					y[1] = be_pair(v[k][0].z & 0xFFFFu, v[k][0].w & 0xFFFFu);
+					y[2] = be_pair(v[k][LPS - 1].x & 0xFFFFu, v[k][LPS - 1].y & 0xFFFFu);
+					y[3] = be_pair(v[k][LPS - 1].z & 0xFFFFu, v[k][LPS - 1].w & 0xFFFFu);
+				}
+			} else {
+#pragma unroll
+				for (uint32_t qq = 0; qq < 4u; qq++)
+					y[qq] = be_pair(sample_at<W>(f, 8u * r + 2u * qq), sample_at<W>(f, 8u * r + 2u * qq + 1u));
+			}
+			// row rb = rr / 4, column chain ^ (rb mod 16): the 64 lanes of a
+			// store (64 consecutive rounds of one frame) hit 64 banks
+#pragma unroll
+			for (uint32_t qq = 0; qq < 4u; qq++)
+				R[((rr >> 2) * 64u + ((fl * 4u + qq) ^ ((rr >> 2) & 15u))) * 4u + (rr & 3u)] = y[qq] * XP2;
+		}
+	};
+
+	const uint32_t q = lane & 3u, fl = lane >> 2;
+	const uint32_t seed = 419764627u;
+	uint32_t acc = q == 0 ? seed + XP1 + XP2 : q == 1 ? seed + XP2 : q == 2 ? seed : seed - XP1;
+	if (wid != 0 && nslots)
+		produce(0);
+	__syncthreads();
+	for (uint32_t sl = 0; sl < nslots; sl++) {
+		if (wid == 0 && AIRS_CK_ABL != 2) {
+			const uint32_t nr = min(CK_RS, stripes - sl * CK_RS);
+			const uint4 *Rs = &ring[sl & 1u][0][0];
+			uint32_t rb = 0;
+			// 16 rounds per step, the next step's inputs read from LDS before
+			// this step's chain runs (the LDS latency stays off the chain)
+			if (16u <= nr) {
+				uint4 cur[4];
+#pragma unroll
+				for (uint32_t u = 0; u < 4u; u++)
+					cur[u] = Rs[u * 64u + (lane ^ u)];
+				for (; 4u * rb + 16u <= nr; rb += 4u) {
+					uint4 nxt[4];
+					// (past the slot's last step: a valid LDS row, value unused)
+#pragma unroll
+					for (uint32_t u = 0; u < 4u; u++)
+						{
+						const uint32_t row = min(rb + 4u + u, CK_RS / 4u - 1u);
+						nxt[u] = Rs[row * 64u + (lane ^ (row & 15u))];
+					}
+#pragma unroll
+					for (uint32_t u = 0; u < 4u; u++) {
+						acc = xxh_round_pre(acc, cur[u].x);
+						acc = xxh_round_pre(acc, cur[u].y);
+						acc = xxh_round_pre(acc, cur[u].z);
+						acc = xxh_round_pre(acc, cur[u].w);
+					}
+#pragma unroll
+					for (uint32_t u = 0; u < 4u; u++)
+						cur[u] = nxt[u];
+				}
+			}
+			for (; 4u * rb + 4u <= nr; rb++) {
+				const uint4 v = Rs[rb * 64u + (lane ^ (rb & 15u))];
+				acc = xxh_round_pre(acc, v.x);
+				acc = xxh_round_pre(acc, v.y);
+				acc = xxh_round_pre(acc, v.z);
+				acc = xxh_round_pre(acc, v.w);
+			}
+			if (4u * rb < nr) {
+				const uint4 v = Rs[rb * 64u + (lane ^ (rb & 15u))];
+				const uint32_t left = nr - 4u * rb;
+				acc = xxh_round_pre(acc, v.x);
+				if (left > 1u)
+					acc = xxh_round_pre(acc, v.y);
+				if (left > 2u)
+					acc = xxh_round_pre(acc, v.z);
+			}
+		} else if (sl + 1u < nslots) {
+			produce(sl + 1u);
+		}
+		__syncthreads();
+	}
+	if (wid != 0 || fl >= nloc)
+		return;
+	// tail of the frame: as checksum_kernel
+	const uint8_t *f = reinterpret_cast<const uint8_t *>((uintptr_t)s_fbase[fl]);
+	const uint32_t a1 = __shfl_down(acc, 1, 4), a2 = __shfl_down(acc, 2, 4), a3 = __shfl_down(acc, 3, 4);
+	if (q != 0)
+		return;
+	uint32_t h = stripes ? rotl32(acc, 1) + rotl32(a1, 7) + rotl32(a2, 12) + rotl32(a3, 18) : seed + XP5;
+	h += len;
+	uint32_t i = 8u * stripes;
+	const uint32_t rem_bytes = len - 16u * stripes;
+	uint32_t b = 0;
+	for (; b + 4u <= rem_bytes; b += 4u, i += 2u)
+		h = rotl32(h + be_pair(sample_at<W>(f, i), sample_at<W>(f, i + 1u)) * XP3, 17) * XP4;
+	if (b < rem_bytes) {
+		const uint32_t s0 = sample_at<W>(f, i);
+		h = rotl32(h + ((s0 >> 8) & 0xFFu) * XP5, 11) * XP1;
+		h = rotl32(h + (s0 & 0xFFu) * XP5, 11) * XP1;
+	}
+	h ^= h >> 15;
+	h *= XP2;
+	h ^= h >> 13;
+	h *= XP3;
+	h ^= h >> 16;
+	const uint32_t lfg = blockIdx.x * 16u + fl;
+	out[frame_list ? frame_list[lfg] : lfg] = h;
+}
+
 // ---------------------------------------------------------------------
 // Per-frame Rice parameter selection (build-defined rule; oracle
 // orc_select_rice_k): total_k = n(k+1) + sum_i min(v_i >> k, 16), v = m + 1.
@@ -1360,12 +1547,27 @@ extern "C" uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src
 	if (!e || !n || !num_frames)
 		return ERRV(E_GENERIC);
 	dim3 grid((num_frames + 15) / 16);
-	if (sample_bytes == 2)
-		hipLaunchKernelGGL(checksum_kernel<2>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
+	// checksum_pc_kernel (producer/consumer) measured slower than the
+	// single-wave kernel: experiment switch AIRS_CK_PC=1
+	static int pc = -1;
+	if (pc < 0) {
+		const char *v = getenv("AIRS_CK_PC");
+		pc = v ? atoi(v) : 0;
+	}
+	if (!pc) {
+		if (sample_bytes == 2)
+			hipLaunchKernelGGL(checksum_kernel<2>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
+					   src_stride, n, num_frames, frame_list, out);
+		else
+			hipLaunchKernelGGL(checksum_kernel<4>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
+					   src_stride, n, num_frames, frame_list, out);
+	} else if (sample_bytes == 2) {
+		hipLaunchKernelGGL(checksum_pc_kernel<2>, grid, dim3(256), 0, e->stream, (const uint8_t *)src,
 				   src_stride, n, num_frames, frame_list, out);
-	else
-		hipLaunchKernelGGL(checksum_kernel<4>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
+	} else {
+		hipLaunchKernelGGL(checksum_pc_kernel<4>, grid, dim3(256), 0, e->stream, (const uint8_t *)src,
 				   src_stride, n, num_frames, frame_list, out);
+	}
 	HIPCHECK(hipGetLastError());
 	return 0;
 }
