@@ -523,6 +523,115 @@ __device__ __forceinline__ uint32_t xxh_round_pre(uint32_t acc, uint32_t yp2)
 	return acc;
 }
 
+// XXH32 in two launches (the default): ck_pre_kernel forms every stripe's
+// four inputs x P2 (the big-endian words of the samples, multiplied off the
+// chain) into a scratch buffer, plane (frame, accumulator q) by plane, with
+// all the parallelism of the frame; ck_chain_kernel then runs only the 64
+// serial chains of 16 frames per wave, reading its inputs 64 rounds ahead.
+// Y holds num_frames x 4 planes of S4 = stripes rounded up to 4 words.
+template <int W>
+__global__ __launch_bounds__(256) void ck_pre_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
+						     uint32_t num_frames, const uint32_t *frame_list, uint32_t S4,
+						     uint32_t *Y)
+{
+	const uint32_t stripes = n / 8u;
+	const uint32_t lf = blockIdx.x;
+	const uint32_t r = blockIdx.y * 256u + threadIdx.x;
+	if (lf >= num_frames || r >= stripes)
+		return;
+	const uint32_t frame = frame_list ? frame_list[lf] : lf;
+	const uint8_t *f = src + (uint64_t)frame * stride;
+	uint32_t y[4];
+	if (W == 2 && ((uintptr_t)f & 15u) == 0u) {
+		const uint4 v = reinterpret_cast<const uint4 *>(f)[r];
+		y[0] = __builtin_amdgcn_perm(v.x, v.x, 0x02030001u);
+		y[1] = __builtin_amdgcn_perm(v.y, v.y, 0x02030001u);
+		y[2] = __builtin_amdgcn_perm(v.z, v.z, 0x02030001u);
+		y[3] = __builtin_amdgcn_perm(v.w, v.w, 0x02030001u);
+	} else if (W == 4 && ((uintptr_t)f & 15u) == 0u) {
+		const uint4 a = reinterpret_cast<const uint4 *>(f)[2u * r];
+		const uint4 b = reinterpret_cast<const uint4 *>(f)[2u * r + 1u];
+		y[0] = be_pair(a.x & 0xFFFFu, a.y & 0xFFFFu);
+		y[1] = be_pair(a.z & 0xFFFFu, a.w & 0xFFFFu);
+		y[2] = be_pair(b.x & 0xFFFFu, b.y & 0xFFFFu);
+		y[3] = be_pair(b.z & 0xFFFFu, b.w & 0xFFFFu);
+	} else {
+#pragma unroll
+		for (uint32_t q = 0; q < 4u; q++)
+			y[q] = be_pair(sample_at<W>(f, 8u * r + 2u * q), sample_at<W>(f, 8u * r + 2u * q + 1u));
+	}
+#pragma unroll
+	for (uint32_t q = 0; q < 4u; q++)
+		Y[((uint64_t)lf * 4u + q) * S4 + r] = y[q] * XP2;
+}
+
+template <int W>
+__global__ __launch_bounds__(64) void ck_chain_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
+						      uint32_t num_frames, const uint32_t *frame_list, uint32_t S4,
+						      const uint32_t *Y, uint32_t *out)
+{
+	const uint32_t lane = threadIdx.x, q = lane & 3u;
+	const uint32_t lf = blockIdx.x * 16u + (lane >> 2);
+	const bool valid = lf < num_frames;
+	const uint32_t len = 2u * n;
+	const uint32_t stripes = len >= 16u ? n / 8u : 0u;
+	const uint32_t seed = 419764627u;
+	uint32_t acc = q == 0 ? seed + XP1 + XP2 : q == 1 ? seed + XP2 : q == 2 ? seed : seed - XP1;
+	const uint4 *P = reinterpret_cast<const uint4 *>(Y + ((uint64_t)(valid ? lf : 0u) * 4u + q) * S4);
+	// batches of 128 rounds (32 x 16 bytes per lane), the next batch loading
+	// while this one runs
+	constexpr uint32_t B = 32u;
+	const uint32_t nb = stripes / (4u * B);
+	uint4 cur[B], nxt[B];
+	if (nb) {
+#pragma unroll
+		for (uint32_t u = 0; u < B; u++)
+			cur[u] = P[u];
+	}
+	for (uint32_t b = 0; b < nb; b++) {
+		const uint32_t nbase = (b + 1u < nb ? b + 1u : b) * B;
+#pragma unroll
+		for (uint32_t u = 0; u < B; u++)
+			nxt[u] = P[nbase + u];
+#pragma unroll
+		for (uint32_t u = 0; u < B; u++) {
+			acc = xxh_round_pre(acc, cur[u].x);
+			acc = xxh_round_pre(acc, cur[u].y);
+			acc = xxh_round_pre(acc, cur[u].z);
+			acc = xxh_round_pre(acc, cur[u].w);
+		}
+#pragma unroll
+		for (uint32_t u = 0; u < B; u++)
+			cur[u] = nxt[u];
+	}
+	for (uint32_t r = nb * 4u * B; r < stripes; r++)
+		acc = xxh_round_pre(acc, reinterpret_cast<const uint32_t *>(P)[r]);
+	const uint32_t a1 = __shfl_down(acc, 1, 4), a2 = __shfl_down(acc, 2, 4), a3 = __shfl_down(acc, 3, 4);
+	if (q != 0 || !valid)
+		return;
+	const uint32_t frame = frame_list ? frame_list[lf] : lf;
+	const uint8_t *f = src + (uint64_t)frame * stride;
+	uint32_t h = stripes ? rotl32(acc, 1) + rotl32(a1, 7) + rotl32(a2, 12) + rotl32(a3, 18) : seed + XP5;
+	h += len;
+	uint32_t i = 8u * stripes;
+	const uint32_t rem_bytes = len - 16u * stripes;
+	uint32_t bb = 0;
+	for (; bb + 4u <= rem_bytes; bb += 4u, i += 2u)
+		h = rotl32(h + be_pair(sample_at<W>(f, i), sample_at<W>(f, i + 1u)) * XP3, 17) * XP4;
+	if (bb < rem_bytes) {
+		const uint32_t s0 = sample_at<W>(f, i);
+		h = rotl32(h + ((s0 >> 8) & 0xFFu) * XP5, 11) * XP1;
+		h = rotl32(h + (s0 & 0xFFu) * XP5, 11) * XP1;
+	}
+	h ^= h >> 15;
+	h *= XP2;
+	h ^= h >> 13;
+	h *= XP3;
+	h ^= h >> 16;
+	out[frame] = h;
+}
+
+
 // XXH32 with the accumulator chains split from their inputs: one consumer
 // wave runs the 64 serial chains of 16 frames (4 lanes per frame, as
 // checksum_kernel) and does only add, rotate, multiply per round; three
@@ -1547,14 +1656,32 @@ extern "C" uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src
 	if (!e || !n || !num_frames)
 		return ERRV(E_GENERIC);
 	dim3 grid((num_frames + 15) / 16);
-	// checksum_pc_kernel (producer/consumer) measured slower than the
-	// single-wave kernel: experiment switch AIRS_CK_PC=1
-	static int pc = -1;
-	if (pc < 0) {
-		const char *v = getenv("AIRS_CK_PC");
-		pc = v ? atoi(v) : 0;
+	// two launches (ck_pre + ck_chain) by default;
+	// AIRS_CK_ALG=1: the single-wave kernel, 2: the producer/consumer kernel
+	static int alg = -1;
+	if (alg < 0) {
+		const char *v = getenv("AIRS_CK_ALG");
+		alg = v ? atoi(v) : 0;
 	}
-	if (!pc) {
+	const uint32_t stripes = 2u * n >= 16u ? n / 8u : 0u;
+	if (alg == 0 && stripes) {
+		const uint32_t S4 = (stripes + 3u) & ~3u;
+		uint32_t *Y = (uint32_t *)airs_dev_scratch(e, AIRS_NSLOT - 4, (size_t)num_frames * 4u * S4 * 4u);
+		if (!Y)
+			return ERRV(E_GENERIC);
+		const dim3 pg(num_frames, (stripes + 255u) / 256u);
+		if (sample_bytes == 2) {
+			hipLaunchKernelGGL(ck_pre_kernel<2>, pg, dim3(256), 0, e->stream, (const uint8_t *)src, src_stride, n,
+					   num_frames, frame_list, S4, Y);
+			hipLaunchKernelGGL(ck_chain_kernel<2>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
+					   src_stride, n, num_frames, frame_list, S4, (const uint32_t *)Y, out);
+		} else {
+			hipLaunchKernelGGL(ck_pre_kernel<4>, pg, dim3(256), 0, e->stream, (const uint8_t *)src, src_stride, n,
+					   num_frames, frame_list, S4, Y);
+			hipLaunchKernelGGL(ck_chain_kernel<4>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
+					   src_stride, n, num_frames, frame_list, S4, (const uint32_t *)Y, out);
+		}
+	} else if (alg != 2) {
 		if (sample_bytes == 2)
 			hipLaunchKernelGGL(checksum_kernel<2>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
 					   src_stride, n, num_frames, frame_list, out);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Checksum-enabled encode: a bench workload with
-checksum_enabled=1, timed per call with HIP events (AIRS_CK_PC=1 selects
-the producer/consumer checksum kernel for comparison).  usage: ck_bench.py cfg2|cfg4"""
+checksum_enabled=1, timed per call with HIP events (AIRS_CK_ALG=1|2 selects
+the single-wave or the producer/consumer checksum kernel for comparison).  usage: ck_bench.py cfg2|cfg4"""
 import json
 import os
 import sys
@@ -42,5 +42,5 @@ for k in range(5):
 e1.record(stream)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / 5
-print(json.dumps(dict(workload=name, checksum=True, pc_kernel=os.environ.get("AIRS_CK_PC", "0"),
+print(json.dumps(dict(workload=name, checksum=True, alg=os.environ.get("AIRS_CK_ALG", "0"),
                       ms_per_call=round(ms, 4), GBps=round(nf * 2 * n / (ms * 1e-3) / 1e9, 1))))
