@@ -525,44 +525,63 @@ __device__ __forceinline__ uint32_t xxh_round_pre(uint32_t acc, uint32_t yp2)
 
 // XXH32 in two launches (the default): ck_pre_kernel forms every stripe's
 // four inputs x P2 (the big-endian words of the samples, multiplied off the
-// chain) into a scratch buffer, plane (frame, accumulator q) by plane, with
-// all the parallelism of the frame; ck_chain_kernel then runs only the 64
-// serial chains of 16 frames per wave, reading its inputs 64 rounds ahead.
-// Y holds num_frames x 4 planes of S4 = stripes rounded up to 4 words.
+// chain) into a scratch buffer with all the parallelism of the frame;
+// ck_chain_kernel then runs only the 64 serial chains of 16 frames per wave,
+// reading its inputs 128 rounds ahead.  Y is laid out for the chain wave:
+// per group of 16 frames, for every 4 rounds, 64 chains x 16 bytes
+// (chain = 4 (frame % 16) + accumulator), so one 16-byte load per lane reads
+// 1 KiB contiguous.  S4 = stripes rounded up to 4.
 template <int W>
 __global__ __launch_bounds__(256) void ck_pre_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
 						     uint32_t num_frames, const uint32_t *frame_list, uint32_t S4,
 						     uint32_t *Y)
 {
+	// a workgroup covers 16 frames x 16 round quads, frame fastest: the 64
+	// lanes of a wave write 4 KiB of Y contiguous (their four stores fill it)
 	const uint32_t stripes = n / 8u;
-	const uint32_t lf = blockIdx.x;
-	const uint32_t r = blockIdx.y * 256u + threadIdx.x;
-	if (lf >= num_frames || r >= stripes)
+	const uint32_t lf = blockIdx.x * 16u + (threadIdx.x & 15u);
+	if (lf >= num_frames)
 		return;
 	const uint32_t frame = frame_list ? frame_list[lf] : lf;
 	const uint8_t *f = src + (uint64_t)frame * stride;
-	uint32_t y[4];
-	if (W == 2 && ((uintptr_t)f & 15u) == 0u) {
-		const uint4 v = reinterpret_cast<const uint4 *>(f)[r];
-		y[0] = __builtin_amdgcn_perm(v.x, v.x, 0x02030001u);
-		y[1] = __builtin_amdgcn_perm(v.y, v.y, 0x02030001u);
-		y[2] = __builtin_amdgcn_perm(v.z, v.z, 0x02030001u);
-		y[3] = __builtin_amdgcn_perm(v.w, v.w, 0x02030001u);
-	} else if (W == 4 && ((uintptr_t)f & 15u) == 0u) {
-		const uint4 a = reinterpret_cast<const uint4 *>(f)[2u * r];
-		const uint4 b = reinterpret_cast<const uint4 *>(f)[2u * r + 1u];
-		y[0] = be_pair(a.x & 0xFFFFu, a.y & 0xFFFFu);
-		y[1] = be_pair(a.z & 0xFFFFu, a.w & 0xFFFFu);
-		y[2] = be_pair(b.x & 0xFFFFu, b.y & 0xFFFFu);
-		y[3] = be_pair(b.z & 0xFFFFu, b.w & 0xFFFFu);
-	} else {
+	// rounds 4 r4 .. 4 r4 + 3 (grid-stride: gridDim.y is capped)
+	for (uint32_t r4 = blockIdx.y * 16u + (threadIdx.x >> 4); 4u * r4 < stripes; r4 += gridDim.y * 16u) {
+		uint32_t y[4][4]; // [round][accumulator]
+		if (4u * r4 + 4u <= stripes && ((uintptr_t)f & 15u) == 0u) {
+#pragma unroll
+			for (uint32_t t = 0; t < 4u; t++) {
+				const uint32_t r = 4u * r4 + t;
+				if (W == 2) {
+					const uint4 v = reinterpret_cast<const uint4 *>(f)[r];
+					y[t][0] = __builtin_amdgcn_perm(v.x, v.x, 0x02030001u);
+					y[t][1] = __builtin_amdgcn_perm(v.y, v.y, 0x02030001u);
+					y[t][2] = __builtin_amdgcn_perm(v.z, v.z, 0x02030001u);
+					y[t][3] = __builtin_amdgcn_perm(v.w, v.w, 0x02030001u);
+				} else {
+					const uint4 a = reinterpret_cast<const uint4 *>(f)[2u * r];
+					const uint4 b = reinterpret_cast<const uint4 *>(f)[2u * r + 1u];
+					y[t][0] = be_pair(a.x & 0xFFFFu, a.y & 0xFFFFu);
+					y[t][1] = be_pair(a.z & 0xFFFFu, a.w & 0xFFFFu);
+					y[t][2] = be_pair(b.x & 0xFFFFu, b.y & 0xFFFFu);
+					y[t][3] = be_pair(b.z & 0xFFFFu, b.w & 0xFFFFu);
+				}
+			}
+		} else {
+#pragma unroll
+			for (uint32_t t = 0; t < 4u; t++) {
+				const uint32_t r = 4u * r4 + t;
+#pragma unroll
+				for (uint32_t q = 0; q < 4u; q++)
+					y[t][q] = r < stripes ? be_pair(sample_at<W>(f, 8u * r + 2u * q),
+								     sample_at<W>(f, 8u * r + 2u * q + 1u))
+							   : 0u;
+			}
+		}
+		uint4 *G = reinterpret_cast<uint4 *>(Y + (uint64_t)(lf >> 4) * 64u * S4) + (uint64_t)r4 * 64u + (lf & 15u) * 4u;
 #pragma unroll
 		for (uint32_t q = 0; q < 4u; q++)
-			y[q] = be_pair(sample_at<W>(f, 8u * r + 2u * q), sample_at<W>(f, 8u * r + 2u * q + 1u));
+			G[q] = make_uint4(y[0][q] * XP2, y[1][q] * XP2, y[2][q] * XP2, y[3][q] * XP2);
 	}
-#pragma unroll
-	for (uint32_t q = 0; q < 4u; q++)
-		Y[((uint64_t)lf * 4u + q) * S4 + r] = y[q] * XP2;
 }
 
 template <int W>
@@ -577,7 +596,8 @@ __global__ __launch_bounds__(64) void ck_chain_kernel(const uint8_t *src, uint64
 	const uint32_t stripes = len >= 16u ? n / 8u : 0u;
 	const uint32_t seed = 419764627u;
 	uint32_t acc = q == 0 ? seed + XP1 + XP2 : q == 1 ? seed + XP2 : q == 2 ? seed : seed - XP1;
-	const uint4 *P = reinterpret_cast<const uint4 *>(Y + ((uint64_t)(valid ? lf : 0u) * 4u + q) * S4);
+	// this lane's chain: 16 bytes (4 rounds) every 1 KiB of its group
+	const uint4 *P = reinterpret_cast<const uint4 *>(Y + (uint64_t)blockIdx.x * 64u * S4) + lane;
 	// batches of 128 rounds (32 x 16 bytes per lane), the next batch loading
 	// while this one runs
 	constexpr uint32_t B = 32u;
@@ -586,13 +606,13 @@ __global__ __launch_bounds__(64) void ck_chain_kernel(const uint8_t *src, uint64
 	if (nb) {
 #pragma unroll
 		for (uint32_t u = 0; u < B; u++)
-			cur[u] = P[u];
+			cur[u] = P[64u * u];
 	}
 	for (uint32_t b = 0; b < nb; b++) {
 		const uint32_t nbase = (b + 1u < nb ? b + 1u : b) * B;
 #pragma unroll
 		for (uint32_t u = 0; u < B; u++)
-			nxt[u] = P[nbase + u];
+			nxt[u] = P[64u * (nbase + u)];
 #pragma unroll
 		for (uint32_t u = 0; u < B; u++) {
 			acc = xxh_round_pre(acc, cur[u].x);
@@ -605,7 +625,7 @@ __global__ __launch_bounds__(64) void ck_chain_kernel(const uint8_t *src, uint64
 			cur[u] = nxt[u];
 	}
 	for (uint32_t r = nb * 4u * B; r < stripes; r++)
-		acc = xxh_round_pre(acc, reinterpret_cast<const uint32_t *>(P)[r]);
+		acc = xxh_round_pre(acc, reinterpret_cast<const uint32_t *>(P + 64u * (r >> 2))[r & 3u]);
 	const uint32_t a1 = __shfl_down(acc, 1, 4), a2 = __shfl_down(acc, 2, 4), a3 = __shfl_down(acc, 3, 4);
 	if (q != 0 || !valid)
 		return;
@@ -1666,10 +1686,11 @@ extern "C" uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src
 	const uint32_t stripes = 2u * n >= 16u ? n / 8u : 0u;
 	if (alg == 0 && stripes) {
 		const uint32_t S4 = (stripes + 3u) & ~3u;
-		uint32_t *Y = (uint32_t *)airs_dev_scratch(e, AIRS_NSLOT - 4, (size_t)num_frames * 4u * S4 * 4u);
+		// whole groups of 16 frames x 4 chains
+		uint32_t *Y = (uint32_t *)airs_dev_scratch(e, AIRS_NSLOT - 4, (size_t)grid.x * 64u * S4 * 4u);
 		if (!Y)
 			return ERRV(E_GENERIC);
-		const dim3 pg(num_frames, (stripes + 255u) / 256u);
+		const dim3 pg(grid.x, min((S4 / 4u + 15u) / 16u, 65535u));
 		if (sample_bytes == 2) {
 			hipLaunchKernelGGL(ck_pre_kernel<2>, pg, dim3(256), 0, e->stream, (const uint8_t *)src, src_stride, n,
 					   num_frames, frame_list, S4, Y);
