@@ -156,8 +156,8 @@ uint32_t airs_dev_synth(struct airs_dev_engine *e, void *dst, uint32_t sample_by
 			uint32_t W);
 
 /* engine-owned scratch, grown on demand (stream ordered) */
-#define AIRS_NSLOT 14 /* scratch slots per engine; the last four are the device layer's
-		       * (checksum products, decoder parse arrays, decoder frame info, IWT heads) */
+#define AIRS_NSLOT 15 /* scratch slots per engine; the last five are the device layer's (checksum
+		       * placement, checksum products, decoder parse arrays, decoder frame info, IWT heads) */
 void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes);
 
 /* rewrite header bytes 8..13 (identifier) of launch frames whose status is

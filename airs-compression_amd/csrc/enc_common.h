@@ -50,6 +50,7 @@ struct KArgs {
 	const uint32_t *frame_list;
 	const uint32_t *frame_g;
 	const uint32_t *checksums;
+	uint32_t *ck_at; // checksum overlapped (airs_dev_encode): payload bytes per launch frame, bytes stored later
 	const uint64_t *ids;
 	uint32_t *status;
 	uint32_t *needed;

@@ -1037,7 +1037,9 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 		const uint32_t endbit = P + A;
 		const uint32_t payload_bytes = (endbit + 7u) >> 3;
 		const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
-		if (a.checksum) {
+		if (a.checksum && a.ck_at) {
+			a.ck_at[lf] = payload_bytes; // ck_emit_kernel stores the checksum once it is done
+		} else if (a.checksum) {
 			const uint32_t ck = a.checksums[frame];
 			for (uint32_t b = 0; b < 4u; b++)
 				if (payload_bytes + b < cap)

@@ -652,6 +652,27 @@ __global__ __launch_bounds__(64) void ck_chain_kernel(const uint8_t *src, uint64
 }
 
 
+// The checksum bytes of an encode launch whose checksums ran on the second
+// stream (airs_dev_encode): the kernel's epilogue left each frame's payload
+// bytes in ck_at; the bytes that fit the capacity follow the payload, as the
+// epilogue stores them otherwise (reference cmp.c:386-390).
+__global__ __launch_bounds__(256) void ck_emit_kernel(uint8_t *dst, uint64_t dst_stride, uint32_t cap,
+						      uint32_t num_frames, const uint32_t *frame_list, uint32_t frame_add,
+						      uint32_t frame_mul, const uint32_t *ck_at, const uint32_t *checksums)
+{
+	const uint32_t lf = blockIdx.x * 256u + threadIdx.x;
+	if (lf >= num_frames)
+		return;
+	const uint32_t frame = frame_list ? frame_list[lf] : frame_add + lf * frame_mul;
+	if (frame == AIRS_NO_FRAME)
+		return;
+	const uint32_t pb = ck_at[lf], ck = checksums[frame];
+	uint8_t *fdst = dst + (uint64_t)frame * dst_stride;
+	for (uint32_t b = 0; b < 4u; b++)
+		if (pb + b < cap)
+			fdst[pb + b] = (uint8_t)(ck >> (24u - 8u * b));
+}
+
 // XXH32 with the accumulator chains split from their inputs: one consumer
 // wave runs the 64 serial chains of 16 frames (4 lanes per frame, as
 // checksum_kernel) and does only add, rotate, multiply per round; three
@@ -1173,7 +1194,22 @@ struct airs_dev_engine {
 	size_t dbgts_n;
 	uint64_t *ktot; // fused Rice selection: 16 candidate granules per segment
 	size_t ktot_cap;
+	// checksums run on a second stream, overlapped with the encode
+	// (airs_dev_checksum); ck_pending = the output of the one not yet joined
+	hipStream_t ck_stream;
+	hipEvent_t ck_ready, ck_done;
+	const uint32_t *ck_pending;
 };
+
+// the main stream waits for the pending checksum (every consumer of the
+// checksums, or of the main stream's results, comes after this)
+static void ck_join(airs_dev_engine *e)
+{
+	if (e->ck_pending) {
+		(void)hipStreamWaitEvent(e->stream, e->ck_done, 0);
+		e->ck_pending = nullptr;
+	}
+}
 
 extern "C" int airs_dev_available(void)
 {
@@ -1203,6 +1239,14 @@ extern "C" struct airs_dev_engine *airs_dev_engine_create(void *stream)
 		return nullptr;
 	}
 	e->epoch = 0;
+	if (hipStreamCreateWithFlags(&e->ck_stream, hipStreamNonBlocking) != hipSuccess ||
+	    hipEventCreateWithFlags(&e->ck_ready, hipEventDisableTiming) != hipSuccess ||
+	    hipEventCreateWithFlags(&e->ck_done, hipEventDisableTiming) != hipSuccess) {
+		snprintf(g_err, sizeof(g_err), "stream/event creation failed");
+		(void)hipFree(e->ticket);
+		free(e);
+		return nullptr;
+	}
 	return e;
 }
 
@@ -1210,7 +1254,12 @@ extern "C" void airs_dev_engine_destroy(struct airs_dev_engine *e)
 {
 	if (!e)
 		return;
+	ck_join(e);
 	(void)hipStreamSynchronize(e->stream);
+	(void)hipStreamSynchronize(e->ck_stream);
+	(void)hipEventDestroy(e->ck_ready);
+	(void)hipEventDestroy(e->ck_done);
+	(void)hipStreamDestroy(e->ck_stream);
 	(void)hipFree(e->agg);
 	(void)hipFree(e->tail);
 	(void)hipFree(e->ticket);
@@ -1232,6 +1281,7 @@ extern "C" void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t by
 		return nullptr;
 	if (e->scratch_cap[slot] < bytes) {
 		(void)hipStreamSynchronize(e->stream);
+		(void)hipStreamSynchronize(e->ck_stream);
 		(void)hipFree(e->scratch[slot]);
 		e->scratch[slot] = nullptr;
 		e->scratch_cap[slot] = 0;
@@ -1502,6 +1552,16 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	uint32_t r = ensure_granules(e, (size_t)segs);
 	if (r)
 		return r;
+	// checksums still running on the second stream: this launch leaves their
+	// bytes to ck_emit_kernel and overlaps them; anything else waits for them
+	uint32_t *ck_at = nullptr;
+	if (e->ck_pending && L->checksum_enabled && L->checksums == e->ck_pending && !pipe) {
+		ck_at = (uint32_t *)airs_dev_scratch(e, AIRS_NSLOT - 5, (size_t)L->num_frames * 4u);
+		if (!ck_at)
+			return ERRV(E_GENERIC);
+	} else {
+		ck_join(e);
+	}
 	// CMP_GPU_AUTO_RICE: fused into the encode kernel for frames of a few
 	// segments without a model; otherwise select_rice_kernel writes g first
 	const bool auto_fused = L->auto_rice && !pipe && L->encoder_type == ENC_ZERO &&
@@ -1540,6 +1600,7 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	k.ktot = auto_fused ? e->ktot : nullptr;
 	k.seqs = L->seqs;
 	k.checksums = L->checksums;
+	k.ck_at = ck_at;
 	k.ids = L->ids;
 	k.status = L->status;
 	k.needed = L->needed;
@@ -1622,6 +1683,13 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 			dispatch_pre<4>(k, L->preprocessing, L->encoder_type, rice, full, L->model_mode, grid, e->stream);
 	}
 	HIPCHECK(hipGetLastError());
+	if (ck_at) {
+		ck_join(e);
+		hipLaunchKernelGGL(ck_emit_kernel, dim3((L->num_frames + 255u) / 256u), dim3(256), 0, e->stream, k.dst,
+				   k.dst_stride, k.cap, L->num_frames, k.frame_list, k.frame_add, k.frame_mul, ck_at,
+				   k.checksums);
+		HIPCHECK(hipGetLastError());
+	}
 	if (k.dbg & 4u)
 		e->ticket_base += (uint32_t)segs;
 	return 0;
@@ -1684,6 +1752,16 @@ extern "C" uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src
 		alg = v ? atoi(v) : 0;
 	}
 	const uint32_t stripes = 2u * n >= 16u ? n / 8u : 0u;
+	// AIRS_CK_OVERLAP=1: the chains on a second stream, overlapped with the
+	// next encode launch.  Measured slower (the chain wave,
+	// issue-bound, loses ~8 % beside the encode even on a CU of its own),
+	// so both launches stay on the main stream by default
+	static int overlap = -1;
+	if (overlap < 0) {
+		const char *v = getenv("AIRS_CK_OVERLAP");
+		overlap = v ? atoi(v) : 0;
+	}
+	ck_join(e);
 	if (alg == 0 && stripes) {
 		const uint32_t S4 = (stripes + 3u) & ~3u;
 		// whole groups of 16 frames x 4 chains
@@ -1691,16 +1769,30 @@ extern "C" uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src
 		if (!Y)
 			return ERRV(E_GENERIC);
 		const dim3 pg(grid.x, min((S4 / 4u + 15u) / 16u, 65535u));
-		if (sample_bytes == 2) {
-			hipLaunchKernelGGL(ck_pre_kernel<2>, pg, dim3(256), 0, e->stream, (const uint8_t *)src, src_stride, n,
-					   num_frames, frame_list, S4, Y);
-			hipLaunchKernelGGL(ck_chain_kernel<2>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
-					   src_stride, n, num_frames, frame_list, S4, (const uint32_t *)Y, out);
-		} else {
-			hipLaunchKernelGGL(ck_pre_kernel<4>, pg, dim3(256), 0, e->stream, (const uint8_t *)src, src_stride, n,
-					   num_frames, frame_list, S4, Y);
-			hipLaunchKernelGGL(ck_chain_kernel<4>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
-					   src_stride, n, num_frames, frame_list, S4, (const uint32_t *)Y, out);
+		// the products on the main stream; the chains there too, or on the
+		// second stream (AIRS_CK_OVERLAP=1)
+		if (sample_bytes == 2)
+			hipLaunchKernelGGL(ck_pre_kernel<2>, pg, dim3(256), 0, e->stream, (const uint8_t *)src, src_stride,
+					   n, num_frames, frame_list, S4, Y);
+		else
+			hipLaunchKernelGGL(ck_pre_kernel<4>, pg, dim3(256), 0, e->stream, (const uint8_t *)src, src_stride,
+					   n, num_frames, frame_list, S4, Y);
+		hipStream_t cs = e->stream;
+		if (overlap) {
+			HIPCHECK(hipEventRecord(e->ck_ready, e->stream));
+			HIPCHECK(hipStreamWaitEvent(e->ck_stream, e->ck_ready, 0));
+			cs = e->ck_stream;
+		}
+		if (sample_bytes == 2)
+			hipLaunchKernelGGL(ck_chain_kernel<2>, grid, dim3(64), 0, cs, (const uint8_t *)src, src_stride, n,
+					   num_frames, frame_list, S4, (const uint32_t *)Y, out);
+		else
+			hipLaunchKernelGGL(ck_chain_kernel<4>, grid, dim3(64), 0, cs, (const uint8_t *)src, src_stride, n,
+					   num_frames, frame_list, S4, (const uint32_t *)Y, out);
+		HIPCHECK(hipGetLastError());
+		if (overlap) {
+			HIPCHECK(hipEventRecord(e->ck_done, e->ck_stream));
+			e->ck_pending = out;
 		}
 	} else if (alg != 2) {
 		if (sample_bytes == 2)
@@ -1759,6 +1851,7 @@ extern "C" uint32_t airs_dev_fb_copy(struct airs_dev_engine *e, const struct air
 {
 	if (!e || !s || !s->num_ctx || s->prev < 0 || !s->n)
 		return ERRV(E_GENERIC);
+	ck_join(e); // the fallback frames carry the checksum
 	const dim3 grid(s->num_ctx, (s->n + 2047u) / 2048u);
 	if (s->sample_bytes == 2)
 		hipLaunchKernelGGL(fb_copy_kernel<2>, grid, dim3(256), 0, e->stream, *s);
@@ -1841,6 +1934,7 @@ extern "C" uint32_t airs_dev_d2h(struct airs_dev_engine *e, void *dst, const voi
 {
 	if (!bytes)
 		return 0;
+	ck_join(e);
 	HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream));
 	return 0;
 }
@@ -1856,6 +1950,7 @@ extern "C" uint32_t airs_dev_memset(struct airs_dev_engine *e, void *dst, int v,
 extern "C" uint32_t airs_dev_sync(struct airs_dev_engine *e)
 {
 	uint32_t faults = 0;
+	ck_join(e);
 	HIPCHECK(hipStreamSynchronize(e->stream));
 	HIPCHECK(hipMemcpy(&faults, e->ticket + AIRS_FAULT_WORD, sizeof(faults), hipMemcpyDeviceToHost));
 	{
