@@ -554,6 +554,19 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 	// frame with ~1024 segments in flight (not ~64), so its first round looks
 	// 256 segments back
 	constexpr int LB_WIN = STREAM ? 4 : AIRS_LB_WIN;
+	// Scalar look-back (experiment, AIRS_SLB=1): the first round reads the
+	// 16 newest granules and the tail through the scalar cache path (glc:
+	// no scalar-cache hit) when the look-back starts, instead of vector loads
+	// issued a chunk earlier that queue behind the CU's cold sample loads.
+	// A stale or unpublished granule only means another round (vector).
+#ifndef AIRS_SLB
+#define AIRS_SLB 1
+#endif
+#ifndef AIRS_SLB_N
+#define AIRS_SLB_N 16
+#endif
+	constexpr bool SLB = AIRS_SLB && LBC >= 1 && !AUTOK;
+	constexpr uint32_t SLB_N = AIRS_SLB_N; // 8, 16 or 32 granules
 	uint64_t gv[LB_WIN];
 #pragma unroll
 	for (int w = 0; w < LB_WIN; w++)
@@ -749,7 +762,7 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 		if (LBC >= 1 && c == (AIRS_LBP) && wid == 0 && !is_first && !(DBG(2u))) {
 			if (AUTOK) // only the predecessor's tail: the offset is known
 				tv0 = gran_load(&a.tail[gseg - 1u]);
-			else
+			else if (!SLB || sif < SLB_N)
 				lb_prefetch<LB_WIN>(a, gv, tv0, gseg, first_seg, lane);
 		}
 		uint32_t ln[NPIECE][EPT]; // piece lengths (kept for the MODEL fail_bit check)
@@ -857,9 +870,62 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 				} else if (!is_first) {
 					// round 0 uses the granules fetched before packing; every
 					// round covers LB_WIN windows of 64, newest first
+					const bool slb = SLB && sif >= SLB_N;
+					if (slb) {
+						typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+						// (the addresses in SGPRs: uniform, but not known to be)
+						auto sptr = [](const uint64_t *p) {
+							const uint64_t v = (uint64_t)(uintptr_t)p;
+							const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)v);
+							const uint32_t h = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+							return (const uint64_t *)(uintptr_t)(((uint64_t)h << 32) | l);
+						};
+						const uint64_t *gp = sptr(&a.agg[gseg - SLB_N]);
+						const uint64_t *tp = sptr(&a.tail[gseg - 1u]);
+						// q[b] = granules gseg - SLB_N + 8 b .. + 7; the loads and their
+						// wait in one statement (lgkmcnt also counts LDS operations)
+						u32x16 q[SLB_N / 8u];
+						uint64_t tq;
+						if constexpr (SLB_N == 32u)
+							asm volatile("s_load_dwordx16 %0, %5, 0x0 glc\n\t"
+								     "s_load_dwordx16 %1, %5, 0x40 glc\n\t"
+								     "s_load_dwordx16 %2, %5, 0x80 glc\n\t"
+								     "s_load_dwordx16 %3, %5, 0xc0 glc\n\t"
+								     "s_load_dwordx2 %4, %6, 0x0 glc\n\t"
+								     "s_waitcnt lgkmcnt(0)"
+								     : "=&s"(q[0]), "=&s"(q[1]), "=&s"(q[2]), "=&s"(q[3]), "=&s"(tq)
+								     : "s"(gp), "s"(tp)
+								     : "memory");
+						else if constexpr (SLB_N == 8u)
+							asm volatile("s_load_dwordx16 %0, %2, 0x0 glc\n\t"
+								     "s_load_dwordx2 %1, %3, 0x0 glc\n\t"
+								     "s_waitcnt lgkmcnt(0)"
+								     : "=&s"(q[0]), "=&s"(tq)
+								     : "s"(gp), "s"(tp)
+								     : "memory");
+						else
+							asm volatile("s_load_dwordx16 %0, %3, 0x0 glc\n\t"
+								     "s_load_dwordx16 %1, %3, 0x40 glc\n\t"
+								     "s_load_dwordx2 %2, %4, 0x0 glc\n\t"
+								     "s_waitcnt lgkmcnt(0)"
+								     : "=&s"(q[0]), "=&s"(q[1]), "=&s"(tq)
+								     : "s"(gp), "s"(tp)
+								     : "memory");
+						// granule gseg - SLB_N + i -> lane SLB_N - 1 - i; lanes >= SLB_N read
+						// as unpublished (tag 0): they send the round to the vector path
+						// unless an inclusive granule comes first
+						uint32_t vl = 0u, vh = 0u;
+#pragma unroll
+						for (uint32_t i = 0; i < SLB_N; i++) {
+							vl = lane == SLB_N - 1u - i ? q[i >> 3][2u * (i & 7u)] : vl;
+							vh = lane == SLB_N - 1u - i ? q[i >> 3][2u * (i & 7u) + 1u] : vh;
+						}
+						gv[0] = ((uint64_t)vh << 32) | vl;
+						tv0 = tq;
+					}
 					uint32_t sum = 0u, spins = 0u, lb_rounds = 0u;
 					int64_t j = (int64_t)gseg - 1;
-					int nwin = LB_WIN;
+					int nwin = slb ? 1 : LB_WIN; // the scalar round fills one window
 					bool done = false;
 					while (!done) {
 						lb_rounds++;
