@@ -553,7 +553,10 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 	// look-back windows of 64 granules fetched per round: a stream is one
 	// frame with ~1024 segments in flight (not ~64), so its first round looks
 	// 256 segments back
-	constexpr int LB_WIN = STREAM ? 4 : AIRS_LB_WIN;
+#ifndef AIRS_STREAM_LB_WIN
+#define AIRS_STREAM_LB_WIN 4
+#endif
+	constexpr int LB_WIN = STREAM ? AIRS_STREAM_LB_WIN : AIRS_LB_WIN;
 	// Scalar look-back (experiment, AIRS_SLB=1): the first round reads the
 	// 16 newest granules and the tail through the scalar cache path (glc:
 	// no scalar-cache hit) when the look-back starts, instead of vector loads
