@@ -550,11 +550,13 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 #ifndef AIRS_LB_WIN
 #define AIRS_LB_WIN 1
 #endif
-	// look-back windows of 64 granules fetched per round: a stream is one
-	// frame with ~1024 segments in flight (not ~64), so its first round looks
-	// 256 segments back
+	// look-back windows of 64 granules fetched per round.  A stream is one
+	// frame with ~1024 segments in flight (not ~64); it used four windows
+	// (256 segments back per round), but one window is 12 % faster on the
+	// 64 Mi-sample stream (cold A/B on one box: 64.9 vs 73.5-74.5 us,
+	// DESIGN.md 3.1.2): the extra windows only add loads to the round
 #ifndef AIRS_STREAM_LB_WIN
-#define AIRS_STREAM_LB_WIN 4
+#define AIRS_STREAM_LB_WIN 1
 #endif
 	constexpr int LB_WIN = STREAM ? AIRS_STREAM_LB_WIN : AIRS_LB_WIN;
 	// Scalar look-back (experiment, AIRS_SLB=1): the first round reads the

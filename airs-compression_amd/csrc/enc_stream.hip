@@ -6,8 +6,8 @@
 // (preprocess.c NONE/DIFF -> cmp_encoder_encode_s16 encoder.c:327-378 ->
 // bitstream_writer.h:124-158, bitstream_flush :205-227), over up to
 // AIRS_STREAM_MAX samples.  Its segments form ONE look-back chain (16 Ki
-// segments for 256 Mi samples), so the kernel's first look-back round reads
-// four windows (256 granules) instead of one.
+// segments for 256 Mi samples); its look-back reads one window of 64
+// granules per round, like a frame's (AIRS_STREAM_LB_WIN, enc_kernel.h).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
