@@ -29,9 +29,12 @@ namespace airs {
 #ifndef AIRS_SEG_CH
 #define AIRS_SEG_CH 4
 #endif
+#ifndef AIRS_SEG_CH_WIDE // chunks per segment for i16-in-i32 and MODEL launches
+#define AIRS_SEG_CH_WIDE 2
+#endif
 __host__ __device__ constexpr uint32_t seg_chunks(int W, int MODEL)
 {
-	return (W == 4 || MODEL) ? 2u : AIRS_SEG_CH;
+	return (W == 4 || MODEL) ? AIRS_SEG_CH_WIDE : AIRS_SEG_CH;
 }
 // LDS chunk images per workgroup: with three, the look-back is evaluated
 // after the third chunk's packing (chunks 0 and 1 are stored late)
