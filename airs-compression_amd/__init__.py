@@ -65,6 +65,7 @@ class GpuBatch(ctypes.Structure):
         ("dst_capacity", c_uint32),
         ("sizes", c_void_p),
         ("flags", c_uint32),
+        ("draws", c_void_p),
     ]
 
 
@@ -123,6 +124,7 @@ class GpuEngine:
 
     def __init__(self, lib: AirsLib, stream: int | None = None):
         self.lib = lib
+        self.stream = stream  # raw hipStream_t the engine's work is queued on (None: the null stream)
         h = c_void_p()
         r = lib.lib.cmp_gpu_engine_create(ctypes.byref(h), stream)
         if is_error(r):
@@ -142,11 +144,12 @@ class GpuEngine:
 
     def compress(self, ctxs, frames_per_ctx: int, kind: str, src_ptr: int, src_stride: int,
                  src_size: int, dst_ptr: int, dst_stride: int, dst_capacity: int, sizes_ptr: int,
-                 flags: int = 0) -> int:
-        """cmp_gpu_compress over device pointers; ctxs is a ctypes CmpContext array."""
+                 flags: int = 0, draws_ptr: int | None = None) -> int:
+        """cmp_gpu_compress over device pointers; ctxs is a ctypes CmpContext array.
+        draws_ptr: optional host uint8 array receiving each frame's identifier draws."""
         b = GpuBatch(type=KIND_TO_GPU[kind], src=src_ptr, src_stride=src_stride, src_size=src_size,
                      dst=dst_ptr, dst_stride=dst_stride, dst_capacity=dst_capacity,
-                     sizes=sizes_ptr, flags=flags)
+                     sizes=sizes_ptr, flags=flags, draws=draws_ptr)
         n_ctx = len(ctxs)
         return self.lib.lib.cmp_gpu_compress(self.handle, ctxs, n_ctx, frames_per_ctx, ctypes.byref(b))
 

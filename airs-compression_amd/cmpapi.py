@@ -34,6 +34,10 @@ CMP_CHECKSUM_SIZE = 4
 CMP_HDR_MAX_COMPRESSED_SIZE = (1 << 24) - 1
 CMP_HDR_MAX_ORIGINAL_SIZE = (1 << 24) - 1
 CMP_VERSION_NUMBER = 600
+# cmp_gpu_batch.flags (include/cmp_gpu.h)
+GPU_AUTO_RICE = 0x1
+GPU_HOST_STEPPED = 0x2
+GPU_STEPWISE = 0x4
 
 
 def err_value(name: str) -> int:

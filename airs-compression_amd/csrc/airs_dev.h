@@ -92,6 +92,41 @@ void *airs_dev_engine_stream(struct airs_dev_engine *e);
 /* enqueue one encode launch; returns 0 or a cmp error value (uint32_t)-code */
 uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L);
 
+/* MODEL streams in one launch (enc_walk.hip): context c's frames c*fpc + a
+ * (a = 0 .. fpc-1) in acquisition order, the model of each context kept on
+ * the chip between acquisitions and written to its work buffer once at the
+ * end.  Only for batches whose passes cannot fail or fall back (the host's
+ * asynchronous mode): frame (c, a) is a primary pass when the context's
+ * sequence number before it is 0 or above `iters` (cmp.c:228-248).
+ * Requirements (airs_dev_walk returns CMP_ERR_PARAMS_INVALID otherwise,
+ * nothing launched): n a multiple of 4096; src, src_stride and every model
+ * 16-byte aligned; primary NONE or DIFF; both encoders GOLOMB_ZERO or
+ * GOLOMB_MULTI with g a power of two. */
+struct airs_walk {
+	const void *src;
+	uint64_t src_stride;
+	uint32_t sample_bytes, is_unsigned, n;
+	uint32_t num_ctx, fpc;
+	void *dst;
+	uint64_t dst_stride;
+	uint32_t cap;
+	void *model;              /* context c's model at model + c*model_stride, or model_ptrs[c] */
+	uint64_t model_stride;
+	const uint64_t *model_ptrs;
+	uint32_t pre_p, enc_p, g_p, outl_p; /* primary pass (outl: the user's outlier parameter) */
+	uint32_t enc_s, g_s, outl_s;        /* secondary pass, MODEL preprocessing */
+	uint32_t model_rate, iters;
+	uint32_t seq0;            /* sequence number of every context before the call, or */
+	const uint8_t *seq0s;     /* device [num_ctx] */
+	uint64_t id_base, id_cstep, id_astep; /* identifier of frame (c, a) = base + c cstep + a astep, or */
+	const uint64_t *ids;      /* device [num_ctx * fpc] */
+	uint32_t checksum_enabled;
+	const uint32_t *checksums; /* device [num_ctx * fpc] */
+	uint32_t *status;         /* device [num_ctx * fpc] */
+};
+int airs_dev_walk_supported(const struct airs_walk *w);
+uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_walk *w);
+
 /* payload-only stream (cmp_gpu_encode_stream): the n samples at src (device)
  * as ONE bit stream from bit 0 of dst, no header or checksum; *status
  * (device) = bytes or error value.  NONE/DIFF preprocessing. */

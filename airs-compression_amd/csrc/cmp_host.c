@@ -866,7 +866,11 @@ static uint32_t launch_groups(struct cmp_gpu_engine *eng, struct cmp_context *ct
 		for (k = i; k < cnt; k++) {
 			if (!done[k] && caps[k] == caps[i] && same_pass(&plan[list[k]].p, &plan[list[i]].p) &&
 			    ctx[list[k] / fpc].params.model_rate == ctx[list[i] / fpc].params.model_rate &&
-			    ctx[list[k] / fpc].params.checksum_enabled == ctx[list[i] / fpc].params.checksum_enabled) {
+			    ctx[list[k] / fpc].params.checksum_enabled == ctx[list[i] / fpc].params.checksum_enabled &&
+			    /* batch_launch decides the model fail bit from the
+			     * launch's first context: one fallback setting per launch */
+			    !ctx[list[k] / fpc].params.uncompressed_fallback_enabled ==
+				    !ctx[list[i] / fpc].params.uncompressed_fallback_enabled) {
 				grp[g++] = list[k];
 				done[k] = 1;
 			}
@@ -1001,6 +1005,8 @@ static uint32_t batch_exact(struct cmp_gpu_engine *eng, struct cmp_context *ctx,
 				for (k = 0; k < draws[f]; k++)
 					id = next_identifier();
 				ids[f] = id;
+				if (b->draws)
+					b->draws[f] = (uint8_t)draws[f];
 			}
 			ctx[c].identifier = id;
 		}
@@ -1038,14 +1044,6 @@ out:
  * read-back of the identifier draw counts and context states at the end;
  * identifiers are then drawn in call order and patched into the headers.
  */
-/* AIRS_HOST_EXACT=1 (tests, comparisons): keep the host-stepped exact mode */
-static int host_exact_forced(void)
-{
-	const char *v = getenv("AIRS_HOST_EXACT");
-
-	return v && atoi(v) != 0;
-}
-
 static int same_params(const struct cmp_params *x, const struct cmp_params *y)
 {
 	return x->primary_preprocessing == y->primary_preprocessing &&
@@ -1270,6 +1268,8 @@ static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_contex
 			for (uint32_t k = 0; k < host_draws[f]; k++)
 				id = next_identifier();
 			ids[f] = id;
+			if (b->draws)
+				b->draws[f] = host_draws[f];
 		}
 		ctx[c].identifier = id;
 		ctx[c].sequence_number = (uint8_t)host_state[2u * c];
@@ -1289,6 +1289,162 @@ out:
 	free(host_state);
 	free(host_draws);
 	return e;
+}
+
+/*
+ * MODEL contexts in one launch (airs_dev_walk, enc_walk.hip): every frame of
+ * the batch, acquisition after acquisition, with each context's model kept on
+ * the chip.  Used in the asynchronous mode (no frame can fail or fall back)
+ * when every context has the same parameters with a MODEL secondary pass and
+ * the plan the host replayed is the one the walk's pass rule gives.
+ * Returns 0, an error value, or WALK_NO (not applicable; nothing launched).
+ */
+#define WALK_NO 1u
+static uint32_t batch_walk(struct cmp_gpu_engine *eng, const struct cmp_context *ctx, uint32_t num_ctx, uint32_t fpc,
+			   const struct cmp_gpu_batch *b, const struct frame_plan *plan)
+{
+	struct airs_dev_engine *dev = eng->dev;
+	const struct cmp_params *P = &ctx[0].params;
+	const uint32_t bytes = b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
+	const uint32_t n = b->src_size / bytes, total = num_ctx * fpc;
+	const uint64_t worst = frame_worst(n);
+	struct airs_walk w;
+	uint32_t c, a, e, seq_same = 1, id_aff = 1, m_strided = 1;
+	uint64_t mbase, mstep;
+
+	if (!model_needed(P) || (P->primary_preprocessing != CMP_PREPROCESS_NONE &&
+				 P->primary_preprocessing != CMP_PREPROCESS_DIFF))
+		return WALK_NO;
+	for (c = 0; c < num_ctx; c++)
+		if (!same_params(&ctx[c].params, P))
+			return WALK_NO;
+	memset(&w, 0, sizeof(w));
+	w.src = b->src;
+	w.src_stride = b->src_stride;
+	w.sample_bytes = bytes;
+	w.is_unsigned = b->type == CMP_GPU_U16;
+	w.n = n;
+	w.num_ctx = num_ctx;
+	w.fpc = fpc;
+	w.dst = b->dst;
+	w.dst_stride = b->dst_stride;
+	w.cap = (uint64_t)b->dst_capacity < worst ? b->dst_capacity : (uint32_t)worst;
+	w.pre_p = P->primary_preprocessing;
+	w.enc_p = P->primary_encoder_type;
+	w.g_p = P->primary_encoder_param;
+	w.outl_p = P->primary_encoder_outlier;
+	w.enc_s = P->secondary_encoder_type;
+	w.g_s = P->secondary_encoder_param;
+	w.outl_s = P->secondary_encoder_outlier;
+	w.model_rate = P->model_rate;
+	w.iters = P->secondary_iterations;
+	w.checksum_enabled = P->checksum_enabled ? 1u : 0u;
+	w.status = b->sizes;
+	/* the walk's pass rule (cmp.c:228-248), started from each context's
+	 * first frame, must give the replayed plan frame by frame */
+	for (c = 0; c < num_ctx; c++) {
+		uint32_t sq = plan[c * fpc].p.seq;
+
+		if (sq != plan[0].p.seq)
+			seq_same = 0;
+		for (a = 0; a < fpc; a++) {
+			const struct pass *p = &plan[c * fpc + a].p;
+			const int prim = sq == 0 || sq > w.iters;
+
+			if (p->seq != (prim ? 0u : sq) ||
+			    p->pre != (prim ? w.pre_p : (uint32_t)CMP_PREPROCESS_MODEL) ||
+			    p->enc != (prim ? w.enc_p : w.enc_s) || p->par != (prim ? w.g_p : w.g_s) ||
+			    p->model_mode != (prim ? (uint32_t)AIRS_MODEL_STORE : (uint32_t)AIRS_MODEL_UPDATE))
+				return WALK_NO;
+			sq = prim ? 1u : sq + 1u;
+		}
+	}
+	w.seq0 = plan[0].p.seq;
+	/* model of context c: strided work buffers, or a pointer list */
+	mbase = (uint64_t)(uintptr_t)ctx[0].work_buf;
+	mstep = num_ctx > 1 ? (uint64_t)(uintptr_t)ctx[1].work_buf - mbase : 0;
+	for (c = 0; c < num_ctx && m_strided; c++)
+		m_strided = (uint64_t)(uintptr_t)ctx[c].work_buf == mbase + c * mstep;
+	if (!m_strided)
+		for (c = 0; c < num_ctx; c++)
+			if ((uintptr_t)ctx[c].work_buf & 15u)
+				return WALK_NO;
+	w.model = (void *)(uintptr_t)mbase;
+	w.model_stride = m_strided ? mstep : 0;
+	/* identifiers: base + c cstep + a astep, or a list */
+	w.id_base = plan[0].id;
+	w.id_cstep = num_ctx > 1 ? plan[fpc].id - plan[0].id : 0;
+	w.id_astep = fpc > 1 ? plan[1].id - plan[0].id : 0;
+	for (c = 0; c < num_ctx && id_aff; c++)
+		for (a = 0; a < fpc && id_aff; a++)
+			id_aff = plan[c * fpc + a].id == w.id_base + c * w.id_cstep + a * w.id_astep;
+	{
+		struct airs_walk chk = w;
+
+		if (!m_strided) /* the pointer list is checked for alignment above */
+			chk.model = NULL, chk.model_stride = 0;
+		if (!airs_dev_walk_supported(&chk))
+			return WALK_NO;
+	}
+	/* device copies of what is not affine; the stream is synchronised before
+	 * the host arrays are freed */
+	if (!m_strided || !id_aff || !seq_same) {
+		uint64_t *d_ptr = NULL, *d_ids = NULL, *h_ptr = NULL, *h_ids = NULL;
+		uint8_t *d_seq = NULL, *h_seq = NULL;
+
+		e = 0;
+		if (!m_strided) {
+			h_ptr = malloc((size_t)num_ctx * 8u);
+			d_ptr = airs_dev_scratch(dev, SLOT_AUX, (size_t)num_ctx * 8u);
+			if (!h_ptr || !d_ptr)
+				e = ERRV(GENERIC);
+			for (c = 0; c < num_ctx && !is_err(e); c++)
+				h_ptr[c] = (uint64_t)(uintptr_t)ctx[c].work_buf;
+			if (!is_err(e))
+				e = airs_dev_h2d(dev, d_ptr, h_ptr, (size_t)num_ctx * 8u);
+			w.model_ptrs = d_ptr;
+		}
+		if (!id_aff && !is_err(e)) {
+			h_ids = malloc((size_t)total * 8u);
+			d_ids = airs_dev_scratch(dev, SLOT_IDS, (size_t)total * 8u);
+			if (!h_ids || !d_ids)
+				e = ERRV(GENERIC);
+			for (c = 0; c < total && !is_err(e); c++)
+				h_ids[c] = plan[c].id;
+			if (!is_err(e))
+				e = airs_dev_h2d(dev, d_ids, h_ids, (size_t)total * 8u);
+			w.ids = d_ids;
+		}
+		if (!seq_same && !is_err(e)) {
+			h_seq = malloc(num_ctx);
+			d_seq = airs_dev_scratch(dev, SLOT_FL, num_ctx);
+			if (!h_seq || !d_seq)
+				e = ERRV(GENERIC);
+			for (c = 0; c < num_ctx && !is_err(e); c++)
+				h_seq[c] = (uint8_t)plan[c * fpc].p.seq;
+			if (!is_err(e))
+				e = airs_dev_h2d(dev, d_seq, h_seq, num_ctx);
+			w.seq0s = d_seq;
+		}
+		if (!is_err(e))
+			e = airs_dev_sync(dev);
+		free(h_ptr);
+		free(h_ids);
+		free(h_seq);
+		if (is_err(e))
+			return e;
+	}
+	if (P->checksum_enabled) {
+		uint32_t *d_ck = airs_dev_scratch(dev, SLOT_CK, (size_t)total * 4u);
+
+		if (!d_ck)
+			return ERRV(GENERIC);
+		e = airs_dev_checksum(dev, b->src, b->src_stride, bytes, n, total, NULL, d_ck);
+		if (is_err(e))
+			return e;
+		w.checksums = d_ck;
+	}
+	return airs_dev_walk(dev, &w);
 }
 
 uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx,
@@ -1412,6 +1568,8 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 					for (uint32_t k = 0; k < draws[f]; k++)
 						id = next_identifier();
 					plan[f].id = id;
+					if (b->draws)
+						b->draws[f] = (uint8_t)draws[f];
 				}
 				ctx[c].identifier = id;
 			}
@@ -1423,7 +1581,7 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		struct pass pp, ps;
 
 		memset(&ps, 0, sizeof(ps));
-		if (!host_exact_forced() && device_exact_ok(ctx, num_ctx, b, n, &pp, &ps))
+		if (!(b->flags & CMP_GPU_HOST_STEPPED) && device_exact_ok(ctx, num_ctx, b, n, &pp, &ps))
 			e = batch_device_exact(eng, ctx, num_ctx, fpc, b, &pp, &ps, ids);
 		else
 			e = batch_exact(eng, ctx, num_ctx, fpc, b, plan, ids, ptrs);
@@ -1451,7 +1609,11 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 			uniform = same_pass(&plan[f].p, &plan[0].p);
 		if (uniform && !any_model) {
 			e = batch_launch(eng, ctx, fpc, b, plan, NULL, 0, 1, total, b->dst_capacity, ids, ptrs);
+		} else if (any_model && !(b->flags & CMP_GPU_STEPWISE) &&
+			   (e = batch_walk(eng, ctx, num_ctx, fpc, b, plan)) != WALK_NO) {
+			/* every acquisition in one launch (or an error) */
 		} else {
+			e = 0;
 			/* one launch per acquisition step across the contexts (one per
 			 * pass when contexts are in different states); MODEL contexts
 			 * carry state from one step to the next */

@@ -1,6 +1,6 @@
 // enc_common.h -- declarations and device helpers shared by the encode
-// kernels (encode.hip: the general kernel and the device layer; enc_pipe.hip:
-// the persistent pipelined kernel).  Reference citations as in encode.hip.
+// kernels (encode.hip: the general kernel and the device layer;
+// enc_stream.hip: payload-only streams).  Reference citations as in encode.hip.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -50,7 +50,6 @@ struct KArgs {
 	const uint32_t *frame_list;
 	const uint32_t *frame_g;
 	const uint32_t *checksums;
-	uint32_t *ck_at; // checksum overlapped (airs_dev_encode): payload bytes per launch frame, bytes stored later
 	const uint64_t *ids;
 	uint32_t *status;
 	uint32_t *needed;
@@ -73,6 +72,8 @@ struct KArgs {
 	uint64_t *ktot;
 	// per batch frame header sequence numbers (device-planned launches), else seq
 	const uint8_t *seqs;
+	// blocks of the (non-persistent) grid: segments, or padded AUTO groups
+	uint32_t grid_blocks;
 };
 
 // frame_list entry of a launch position without a frame this launch
@@ -417,16 +418,32 @@ __device__ __forceinline__ void dbg_stamp(const KArgs &a, uint32_t gseg, uint32_
 }
 
 
-// the persistent pipelined kernel (enc_pipe.hip): whole segments of
-// pipe_segn(sample_bytes) samples, no model, NONE or DIFF; k.segs_per_frame /
-// k.num_segs count those segments
 // payload-only streams (enc_stream.hip): one frame of n <= AIRS_STREAM_MAX
 // samples, no header; bit offsets stay below 2^32 at 48 bits per sample
 uint32_t stream_segn(uint32_t sample_bytes);
+// MODEL streams in one launch (enc_walk.hip, airs_walk in airs_dev.h)
+struct WArgs {
+	const uint8_t *src;
+	uint8_t *dst;
+	uint8_t *model;
+	const uint64_t *model_ptrs;
+	const uint32_t *checksums;
+	const uint64_t *ids;
+	const uint8_t *seq0s;
+	uint32_t *status;
+	uint64_t *agg;
+	uint64_t *tail;
+	uint32_t *ticket;
+	uint64_t src_stride, dst_stride, model_stride;
+	uint64_t id_base, id_cstep, id_astep;
+	uint32_t n, spf, num_ctx, fpc;
+	uint32_t cap, iters, seq0, epoch;
+	uint32_t g_p, outl_p, g_s, outl_s;
+	uint32_t model_rate, is_unsigned, checksum, img_words;
+};
+bool walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
+		 bool rice_s, hipStream_t s);
 void stream_encode(const KArgs &k, uint32_t sample_bytes, uint32_t pre, uint32_t enc, bool rice, bool full,
 		   uint32_t grid, hipStream_t s);
-
-uint32_t pipe_segn(uint32_t sample_bytes);
-uint32_t pipe_encode(const KArgs &k, uint32_t sample_bytes, uint32_t pre, uint32_t enc, bool rice, hipStream_t s);
 
 } // namespace airs

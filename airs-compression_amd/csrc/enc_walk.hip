@@ -1,0 +1,539 @@
+// enc_walk.hip -- MODEL streams in one launch (gfx950).
+//
+// A batch whose contexts carry a model (secondary MODEL passes, reference
+// lib/compress/cmp.c:250-254, update :120-142, applied :304-311) encodes its
+// acquisitions in order: frame (c, a+1) reads the model frame (c, a) left.
+// The per-acquisition launches of encode_kernel re-read and rewrite that
+// model from HBM every step (2 B + 2 B per sample).  Here one launch walks
+// every acquisition of every context:
+//
+//   * workgroup (c, j) owns segment j (4096 samples) of context c's frames
+//     and walks a = 0 .. fpc-1; it keeps the model of its samples in
+//     registers (8 packed VGPRs per lane) and writes it to the work buffer
+//     once, after the last acquisition;
+//   * the samples of acquisition a+1 are loaded while acquisition a packs
+//     (registers, issued right after phase 1);
+//   * waves 0-3 are data waves (16 samples per lane); wave 4 is the control
+//     wave: aggregate publish, decoupled look-back over the frame's segments,
+//     predecessor tail, frame epilogue (header, checksum, status).  So the
+//     data waves never wait on granule loads, whose vmcnt would also wait for
+//     their prefetch, and the look-back overlaps their packing;
+//   * each frame is its own look-back chain (segments j of frame c*fpc + a).
+//
+// Pass selection is data-independent here (no fallback, capacity >= worst
+// case: the host's asynchronous mode), so every frame's pass follows from the
+// context's sequence number at the start of the call (cmp.c:228-248):
+// primary when seq == 0 or seq > secondary_iterations.
+//
+// Per-sample coding (reference encoder.c:303-378): Rice codes come from LDS
+// tables, codeword = m + T[idx], length len[idx]:
+//   GOLOMB_ZERO  idx = min((m+1) >> k, 17); the escape (q >= 17) is entry 17
+//   GOLOMB_MULTI idx = m >> k below the outlier; an escape m >= outlier with
+//                d = m - outlier takes idx = 16 + clz(d | 3), whose entry
+//                holds golomb(outlier + lvl) shifted over the 2 (lvl+1) bits
+//                of d (lvl = floor(log2 d) / 2, 0 for d < 4); the codeword is
+//                then m + T as well.  Escapes longer than 32 bits (lvl 7) are
+//                put in two pieces.
+// Other encoders (UNCOMPRESSED, g not a power of two) take code_from_m.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "enc_common.h"
+
+namespace airs {
+
+// rows of the code tables in LDS (one table per pass)
+#define WTAB 48u
+
+// table entry idx of a pass: {T, len}; see the header comment
+template <int ENC>
+__device__ __forceinline__ uint2 walk_table_entry(uint32_t idx, const Coder &c)
+{
+	const uint32_t k = c.k;
+	if (ENC == ENC_ZERO)
+		return rice_table_entry(idx < 17u ? idx : 17u, k);
+	// GOLOMB_MULTI, Rice: g = 2^k
+	auto rice_cw = [&](uint32_t v, uint32_t &len) {
+		const uint32_t q = v >> k;
+		len = q + k + 1u;
+		return (((1u << q) - 1u) << (k + 1u)) | (v & (c.g - 1u));
+	};
+	if (idx < 32u) {
+		// T[q] = (2^q - 1) 2^(k+1) - q 2^k (mod 2^32): m + T[q] = golomb(m)
+		const uint32_t q = idx;
+		const uint32_t t = (q + k + 1u >= 32u ? 0u - (2u << k) : ((1u << (q + k + 1u)) - (2u << k))) - (q << k);
+		return make_uint2(t, q + k + 1u);
+	}
+	const uint32_t tz = idx - 16u; // clz(d | 3) in [16, 30]
+	const uint32_t lvl = (31u - tz) >> 1;
+	uint32_t len1;
+	const uint32_t cw1 = rice_cw(c.outlier + lvl, len1);
+	const uint32_t len2 = 2u * (lvl + 1u);
+	const uint32_t len = len1 + len2;
+	// len > 32: put as two pieces (cw1, then d); T unused
+	return make_uint2(len <= 32u ? (cw1 << len2) - c.outlier : cw1, len);
+}
+
+
+__device__ __forceinline__ void lds_barrier()
+{
+	// LDS-only barrier: the data waves' prefetch stays in flight across it
+	asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// one pass's residual-independent coding: table offsets (8 idx per sample,
+// 16-bit halves of oq[]), lengths total of the lane; returns the lane's bits
+template <int ENC, bool RICE>
+__device__ __forceinline__ uint32_t walk_lengths(const uint32_t (&mp)[EPT / 2], uint32_t (&oq)[EPT / 2],
+						 const Coder &cd, bool fast, const char *tab)
+{
+	uint32_t t = 0u;
+	if (ENC == ENC_ZERO && RICE && fast) {
+		u16x2 acc = (u16x2)(0);
+#pragma unroll
+		for (uint32_t j = 0; j < EPT / 2; j++) {
+			const u16x2 v = __builtin_elementwise_add_sat(pk(mp[j]), (u16x2)(1));
+			const u16x2 q = v >> (u16x2)((unsigned short)cd.k);
+			acc += __builtin_elementwise_min(q, (u16x2)(16));
+			oq[j] = unpk(__builtin_elementwise_min(q, (u16x2)(17)) << (u16x2)(3));
+		}
+		return EPT * (cd.k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
+	}
+	if (ENC == ENC_MULTI && RICE) {
+		const uint32_t om1 = cd.outlier - 1u;
+#pragma unroll
+		for (uint32_t j = 0; j < EPT / 2; j++) {
+			uint32_t o2 = 0u;
+#pragma unroll
+			for (uint32_t h = 0; h < 2u; h++) {
+				const uint32_t m = half16(mp[j], h);
+				const uint32_t qo = (m >> cd.k) << 3;
+				const uint32_t eo = (((uint32_t)__clz((int)((m - cd.outlier) | 3u))) << 3) + 128u;
+				const uint32_t off = m > om1 ? eo : qo;
+				o2 |= off << (16u * h);
+				t += reinterpret_cast<const uint2 *>(tab + off)->y;
+			}
+			oq[j] = o2;
+		}
+		return t;
+	}
+#pragma unroll
+	for (uint32_t j = 0; j < EPT; j++)
+		t += len_from_m<ENC, RICE>(half16(mp[j >> 1], j & 1u), cd);
+	return t;
+}
+
+// pack the lane's 16 codewords from bit `excl` of the image
+template <int ENC, bool RICE>
+__device__ __forceinline__ void walk_pack(uint32_t *img, uint32_t excl, const uint32_t (&mp)[EPT / 2],
+					  const uint32_t (&oq)[EPT / 2], const Coder &cd, bool fast, const char *tab)
+{
+	Packer pk1;
+	pk1.init(img, excl);
+	if (ENC == ENC_ZERO && RICE && fast) {
+#pragma unroll
+		for (uint32_t hb = 0; hb < 2; hb++) { // two batches of 8 lookups (pairs of codewords per put)
+			uint2 te[EPT / 2];
+#pragma unroll
+			for (uint32_t jj = 0; jj < EPT / 4; jj++) {
+				const uint32_t j = hb * (EPT / 4) + jj;
+#pragma unroll
+				for (uint32_t h = 0; h < 2; h++)
+					te[2 * jj + h] = *reinterpret_cast<const uint2 *>(tab + half16(oq[j], h));
+			}
+			uint32_t mxl = 0u;
+#pragma unroll
+			for (uint32_t i = 0; i < EPT / 2; i += 2)
+				mxl = max(mxl, te[i].y + te[i + 1].y);
+			if (__ballot(mxl > 32u) == 0ull) {
+#pragma unroll
+				for (uint32_t i = 0; i < EPT / 2; i += 2) {
+					const uint32_t j = hb * (EPT / 2) + i;
+					const uint32_t cwa = (mp[j >> 1] & 0xFFFFu) + te[i].x;
+					const uint32_t cwb = (mp[j >> 1] >> 16) + te[i + 1].x;
+					pk1.put((cwa << te[i + 1].y) | cwb, te[i].y + te[i + 1].y);
+				}
+			} else {
+#pragma unroll
+				for (uint32_t i = 0; i < EPT / 2; i += 2) {
+					const uint32_t j = hb * (EPT / 2) + i;
+					pk1.put((mp[j >> 1] & 0xFFFFu) + te[i].x, te[i].y);
+					pk1.put((mp[j >> 1] >> 16) + te[i + 1].x, te[i + 1].y);
+				}
+			}
+		}
+	} else if (ENC == ENC_MULTI && RICE) {
+#pragma unroll
+		for (uint32_t j = 0; j < EPT; j++) {
+			const uint32_t m = half16(mp[j >> 1], j & 1u);
+			const uint2 e = *reinterpret_cast<const uint2 *>(tab + half16(oq[j >> 1], j & 1u));
+			if (e.y <= 32u) {
+				pk1.put(m + e.x, e.y);
+			} else { // lvl-7 escape: golomb(outlier + 7), then d in 16 bits
+				pk1.put(e.x, e.y - 16u);
+				pk1.put(m - cd.outlier, 16u);
+			}
+		}
+	} else {
+#pragma unroll
+		for (uint32_t j = 0; j < EPT; j++) {
+			uint32_t c1, l1, c2, l2;
+			code_from_m<ENC, RICE>(half16(mp[j >> 1], j & 1u), cd, c1, l1, c2, l2);
+			pk1.put(c1, l1);
+			if (ENC == ENC_MULTI)
+				pk1.put(c2, l2);
+		}
+	}
+	pk1.flush();
+}
+
+// the frame's first payload dword shares header bytes 20-21 (outlier low half)
+__device__ __forceinline__ uint32_t hdr_bits(int pre, int enc)
+{
+	return (pre == PRE_NONE && enc == ENC_RAW) ? 128u : 176u;
+}
+
+template <int W, int PRE_P, int ENC_P, bool RICE_P, int ENC_S, bool RICE_S>
+__global__ __launch_bounds__(320) void walk_kernel(WArgs a)
+{
+	constexpr uint32_t RW = EPT * W / 16u; // uint4 per lane
+	extern __shared__ __attribute__((aligned(16))) uint32_t L_img[];
+	__shared__ uint32_t s_wsum[4];
+	__shared__ uint32_t s_ctl[4];
+	__shared__ __attribute__((aligned(16))) uint2 s_tab[2][WTAB];
+
+	const uint32_t tid = threadIdx.x, lane = tid & 63u;
+	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const bool data = wid < 4u;
+	const uint32_t c = blockIdx.x / a.spf, j = blockIdx.x - c * a.spf;
+	const bool is_first = j == 0u, is_last = j + 1u == a.spf;
+	const uint32_t n = a.n;
+	const uint32_t first = j * AIRS_SEG + (data ? tid : 0u) * EPT; // lane's first sample
+	uint16_t *mbase = reinterpret_cast<uint16_t *>(a.model_ptrs ? (uint8_t *)(uintptr_t)a.model_ptrs[c]
+								    : a.model + (uint64_t)c * a.model_stride);
+	uint32_t *img = L_img + 4u;
+
+	const Coder cp = make_coder<ENC_P>(ENC_P == ENC_RAW ? 1u : a.g_p, a.outl_p);
+	const Coder cs = make_coder<ENC_S>(ENC_S == ENC_RAW ? 1u : a.g_s, a.outl_s);
+	const bool fast_p = RICE_P && (ENC_P == ENC_MULTI || (ENC_P == ENC_ZERO && cp.k <= 11u));
+	const bool fast_s = RICE_S && (ENC_S == ENC_MULTI || (ENC_S == ENC_ZERO && cs.k <= 11u));
+	if (tid < WTAB) {
+		if (fast_p)
+			s_tab[0][tid] = walk_table_entry<ENC_P>(tid, cp);
+		if (fast_s)
+			s_tab[1][tid] = walk_table_entry<ENC_S>(tid, cs);
+	}
+	for (uint32_t i = tid; i < a.img_words + 4u; i += 320u)
+		L_img[i] = 0u;
+
+	const uint32_t seq0 = a.seq0s ? a.seq0s[c] : a.seq0;
+	// the model of this lane's 16 samples, packed pairs
+	uint32_t mdl[EPT / 2];
+#pragma unroll
+	for (uint32_t q = 0; q < EPT / 2; q++)
+		mdl[q] = 0u;
+	if (data && seq0 != 0u && seq0 <= a.iters) { // the first frame is a secondary pass
+		const uint4 *mp4 = reinterpret_cast<const uint4 *>(mbase + first);
+#pragma unroll
+		for (uint32_t q = 0; q < EPT / 8; q++) {
+			const uint4 v = mp4[q];
+			mdl[4 * q] = v.x;
+			mdl[4 * q + 1] = v.y;
+			mdl[4 * q + 2] = v.z;
+			mdl[4 * q + 3] = v.w;
+		}
+	}
+	// prefetch of acquisition 0
+	uint4 rn[RW];
+	uint32_t pn = 0u;
+	auto issue = [&](uint32_t acq) {
+		const uint8_t *fs = a.src + (uint64_t)(c * a.fpc + acq) * a.src_stride;
+		const uint4 *p = reinterpret_cast<const uint4 *>(fs + (size_t)first * W);
+#pragma unroll
+		for (uint32_t q = 0; q < RW; q++)
+			rn[q] = p[q];
+		if (PRE_P == PRE_DIFF && lane == 0u && first != 0u)
+			pn = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fs)[first - 1u]
+				    : reinterpret_cast<const uint32_t *>(fs)[first - 1u] & 0xFFFFu;
+	};
+	if (data)
+		issue(0u);
+	__syncthreads(); // tables and the zeroed image
+
+	const char *tab_p = reinterpret_cast<const char *>(s_tab[0]);
+	const char *tab_s = reinterpret_cast<const char *>(s_tab[1]);
+	uint32_t sq = seq0;
+	for (uint32_t acq = 0; acq < a.fpc; acq++) {
+		const uint32_t f = c * a.fpc + acq;
+		const bool prim = sq == 0u || sq > a.iters; // cmp.c:228-248
+		const uint32_t hseq = prim ? 0u : sq;
+		sq = prim ? 1u : sq + 1u;
+		const uint32_t HB = prim ? hdr_bits(PRE_P, ENC_P) : hdr_bits(PRE_MODEL, ENC_S);
+		const uint32_t gseg = f * a.spf + j;
+		uint32_t mp[EPT / 2], oq[EPT / 2];
+		uint32_t T = 0u, excl = 0u;
+		if (data) {
+			// ---- phase 1: samples, residuals, model update, lengths ----------
+			uint32_t w[EPT / 2];
+			if (W == 2) {
+#pragma unroll
+				for (uint32_t q = 0; q < RW; q++) {
+					w[4 * q] = rn[q].x;
+					w[4 * q + 1] = rn[q].y;
+					w[4 * q + 2] = rn[q].z;
+					w[4 * q + 3] = rn[q].w;
+				}
+			} else {
+#pragma unroll
+				for (uint32_t q = 0; q < RW; q++) {
+					w[2 * q] = __builtin_amdgcn_perm(rn[q].y, rn[q].x, 0x05040100u);
+					w[2 * q + 1] = __builtin_amdgcn_perm(rn[q].w, rn[q].z, 0x05040100u);
+				}
+			}
+			const uint32_t prevs = pn;
+			if (acq + 1u < a.fpc)
+				issue(acq + 1u); // lands while this acquisition packs
+			if (prim) {
+				uint32_t wprev = 0u;
+				if (PRE_P == PRE_DIFF) {
+					wprev = __shfl_up(w[EPT / 2 - 1], 1, 64);
+					if (lane == 0u)
+						wprev = prevs << 16;
+				}
+#pragma unroll
+				for (uint32_t q = 0; q < EPT / 2; q++) {
+					uint32_t u = w[q];
+					if (PRE_P == PRE_DIFF)
+						u = unpk(pk(w[q]) - pk(__builtin_amdgcn_alignbit(w[q], q ? w[q - 1] : wprev, 16)));
+					mp[q] = ENC_P == ENC_RAW ? u : zigzag_pk(u);
+					mdl[q] = w[q]; // cmp.c:305-306: the model takes the samples
+				}
+				T = walk_lengths<ENC_P, RICE_P>(mp, oq, cp, fast_p, tab_p);
+			} else {
+				const int32_t rate = (int32_t)a.model_rate;
+#pragma unroll
+				for (uint32_t q = 0; q < EPT / 2; q++) {
+					const uint32_t u = unpk(pk(w[q]) - pk(mdl[q])); // preprocess.c:406-411
+					mp[q] = ENC_S == ENC_RAW ? u : zigzag_pk(u);
+					uint32_t nm = 0u; // cmp.c:132-142
+#pragma unroll
+					for (uint32_t h = 0; h < 2u; h++) {
+						const uint32_t xv = half16(w[q], h), mv = half16(mdl[q], h);
+						const int32_t d = a.is_unsigned ? (int32_t)xv : (int32_t)(int16_t)xv;
+						const int32_t mm = a.is_unsigned ? (int32_t)mv : (int32_t)(int16_t)mv;
+						nm |= ((uint32_t)((mm * rate + d * (16 - rate)) >> 4) & 0xFFFFu) << (16u * h);
+					}
+					mdl[q] = nm;
+				}
+				T = walk_lengths<ENC_S, RICE_S>(mp, oq, cs, fast_s, tab_s);
+			}
+#pragma unroll
+			for (uint32_t q = 0; q < EPT / 2; q++)
+				asm volatile("" : "+v"(mp[q]), "+v"(oq[q]));
+			const uint32_t inc = wave_incl_scan(T);
+			if (lane == 63u)
+				s_wsum[wid] = inc;
+			excl = inc - T;
+		}
+		lds_barrier(); // B1: wave totals
+		const uint32_t w0 = s_wsum[0], w1 = s_wsum[1], w2 = s_wsum[2], w3 = s_wsum[3];
+		const uint32_t A = __builtin_amdgcn_readfirstlane(w0 + w1 + w2 + w3);
+		if (data) {
+			excl += (wid > 0u ? w0 : 0u) + (wid > 1u ? w1 : 0u) + (wid > 2u ? w2 : 0u);
+			// ---- pack into the image ----------------------------------------
+			if (prim)
+				walk_pack<ENC_P, RICE_P>(img, excl, mp, oq, cp, fast_p, tab_p);
+			else
+				walk_pack<ENC_S, RICE_S>(img, excl, mp, oq, cs, fast_s, tab_s);
+			if (wid == 3u && !is_last) {
+				// the segment's last 32 bits (wave 3's own lanes wrote them) for
+				// the successor's first word
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+				const uint32_t s0 = A - 32u, qw = s0 >> 5, sh = s0 & 31u;
+				const uint32_t tl = sh ? (img[qw] << sh) | (img[qw + 1u] >> (32u - sh)) : img[qw];
+				if (lane == 0u)
+					gran_store(&a.tail[gseg], ((uint64_t)a.epoch << 32) | tl);
+			}
+		} else {
+			// ---- control wave: aggregate, look-back, predecessor tail --------
+			if (lane == 0u) {
+				const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
+				gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HB + A : A));
+			}
+			uint32_t P = HB, pred = 0u;
+			if (is_first) {
+				const uint32_t enc = prim ? ENC_P : ENC_S;
+				pred = (enc != ENC_RAW) ? ((prim ? cp.outlier : cs.outlier) & 0xFFFFu) : 0u;
+			} else {
+				const uint32_t first_seg = gseg - j;
+				uint32_t sum = 0u, spins = 0u;
+				int64_t jj = (int64_t)gseg - 1;
+				for (;;) {
+					const int64_t idx = jj - (int64_t)lane;
+					const bool inr = idx >= (int64_t)first_seg;
+					const uint64_t gv = inr ? gran_load(&a.agg[idx]) : 0ull;
+					const uint32_t tag = (uint32_t)(gv >> 32);
+					const bool valid = inr && (tag >> 1) == a.epoch;
+					const bool incl = valid && (tag & 1u);
+					const uint64_t incl_m = __ballot(incl);
+					const uint64_t bad_m = __ballot(inr && !valid);
+					const uint32_t fi = incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
+					const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
+					if (bad_m & need) { // a needed predecessor has not published yet
+						if (++spins > AIRS_SPIN_LIMIT) {
+							if (lane == 0)
+								atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+							break;
+						}
+						__builtin_amdgcn_s_sleep(1);
+						continue;
+					}
+					sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv : 0u);
+					if (incl_m)
+						break;
+					jj -= 64;
+				}
+				P = sum;
+				if (lane == 0u)
+					gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (P + A));
+				// the predecessor's last 32 bits (published after its packing)
+				uint64_t tv = 0ull;
+				if (lane == 0u) {
+					uint32_t sp = 0u;
+					for (tv = gran_load(&a.tail[gseg - 1u]); (uint32_t)(tv >> 32) != a.epoch;
+					     tv = gran_load(&a.tail[gseg - 1u])) {
+						if (++sp > AIRS_SPIN_LIMIT) {
+							atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+							break;
+						}
+						__builtin_amdgcn_s_sleep(1);
+					}
+				}
+				pred = (uint32_t)__shfl(tv, 0, 64);
+			}
+			if (lane == 0u) {
+				s_ctl[0] = P;
+				s_ctl[1] = pred;
+			}
+		}
+		lds_barrier(); // B2: packed image, offset and predecessor bits
+		const uint32_t P = __builtin_amdgcn_readfirstlane(s_ctl[0]);
+		const uint32_t pred = __builtin_amdgcn_readfirstlane(s_ctl[1]);
+		const uint32_t r = P & 31u, g0 = P >> 5;
+		const uint32_t endbit = P + A;
+		const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
+		const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
+		uint8_t *fdst = a.dst + (uint64_t)f * a.dst_stride;
+		const __amdgpu_buffer_rsrc_t dst_rsrc =
+			__builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(a.cap & ~3u), 0x00020000);
+		if (data) {
+			// ---- store: funnel shift to the frame bit offset, big-endian ------
+			const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)img);
+			const uint32_t nquad = nfull >> 2;
+			for (uint32_t p = tid; p < nquad; p += 256u) {
+				const uint32_t jw = 4u * p;
+				const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + jw);
+				const uint32_t hi = jw ? Ll[jw - 1u] : pred;
+				u32x4 o;
+				o.x = bswap32(__builtin_amdgcn_alignbit(hi, wv.x, r));
+				o.y = bswap32(__builtin_amdgcn_alignbit(wv.x, wv.y, r));
+				o.z = bswap32(__builtin_amdgcn_alignbit(wv.y, wv.z, r));
+				o.w = bswap32(__builtin_amdgcn_alignbit(wv.z, wv.w, r));
+				__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
+			}
+			const uint32_t rr = (tid - nquad) & 255u;
+			if (rr < (nfull & 3u)) {
+				const uint32_t jw = 4u * nquad + rr;
+				const uint32_t hi = jw ? Ll[jw - 1u] : pred;
+				const uint32_t v = __builtin_amdgcn_alignbit(hi, Ll[jw], r);
+				__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
+			}
+		} else if (is_last && lane == 0u) {
+			// ---- frame epilogue (cmp.c:314-334) ---------------------------------
+			if (nfull == J) { // zero-padded final bytes (bitstream_flush)
+				const uint32_t hi = J ? img[J - 1u] : pred;
+				const uint32_t v = __builtin_amdgcn_alignbit(hi, img[J], r);
+				const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
+				for (uint32_t b = 0; b < nbytes; b++)
+					if (4u * (g0 + J) + b < a.cap)
+						fdst[4u * (g0 + J) + b] = (uint8_t)(v >> (24u - 8u * b));
+			}
+			const uint32_t payload_bytes = (endbit + 7u) >> 3;
+			const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
+			if (a.checksum) {
+				const uint32_t ck = a.checksums[f];
+				for (uint32_t b = 0; b < 4u; b++)
+					if (payload_bytes + b < a.cap)
+						fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
+			}
+			const uint64_t id = a.ids ? a.ids[f] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)acq * a.id_astep;
+			uint32_t h[5];
+			if (prim)
+				header_words(h, size, 2u * n, id, hseq, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
+					     ENC_P == ENC_RAW ? 0u : cp.g, ENC_P == ENC_RAW ? 0u : cp.outlier);
+			else
+				header_words(h, size, 2u * n, id, hseq, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S, a.model_rate,
+					     ENC_S == ENC_RAW ? 0u : cs.g, ENC_S == ENC_RAW ? 0u : cs.outlier);
+			const uint32_t hwords = HB == 176u ? 5u : 4u;
+			for (uint32_t wq = 0; wq < hwords; wq++)
+				if (4u * wq + 4u <= a.cap)
+					*reinterpret_cast<uint32_t *>(fdst + 4u * wq) = bswap32(h[wq]);
+			a.status[f] = size > a.cap ? ERRV(E_DST_TOO_SMALL)
+						   : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
+		}
+		lds_barrier(); // B3: the image was read
+		// clear what this acquisition used (words 0 .. (A+31)/32 - 1, and the
+		// one after for the flush)
+		const uint32_t nw = (A + 63u) >> 5;
+		for (uint32_t i = tid; i < nw; i += 320u)
+			img[i] = 0u;
+		// (the next acquisition's packing comes after its B1)
+	}
+	// the model after the last acquisition, to the work buffer (cmp.c:304-311)
+	if (data) {
+		uint4 *mo = reinterpret_cast<uint4 *>(mbase + first);
+#pragma unroll
+		for (uint32_t q = 0; q < EPT / 8; q++)
+			mo[q] = make_uint4(mdl[4 * q], mdl[4 * q + 1], mdl[4 * q + 2], mdl[4 * q + 3]);
+	}
+}
+
+// ---------------------------------------------------------------------
+// launch (airs_dev_walk, airs_dev.h)
+// ---------------------------------------------------------------------
+template <int W, int PRE_P, int ENC_P, bool RICE_P>
+static bool walk_launch_s(const WArgs &k, uint32_t enc_s, bool rice_s, size_t lds, hipStream_t s)
+{
+	const dim3 grid(k.num_ctx * k.spf), blk(320);
+	if (enc_s == ENC_ZERO && rice_s)
+		hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true>), grid, blk, lds, s, k);
+	else if (enc_s == ENC_MULTI && rice_s)
+		hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true>), grid, blk, lds, s, k);
+	else
+		return false;
+	return true;
+}
+
+template <int W, int PRE_P>
+static bool walk_launch_p(const WArgs &k, uint32_t enc_p, bool rice_p, uint32_t enc_s, bool rice_s, size_t lds,
+			  hipStream_t s)
+{
+	if (enc_p == ENC_ZERO && rice_p)
+		return walk_launch_s<W, PRE_P, ENC_ZERO, true>(k, enc_s, rice_s, lds, s);
+	if (enc_p == ENC_MULTI && rice_p)
+		return walk_launch_s<W, PRE_P, ENC_MULTI, true>(k, enc_s, rice_s, lds, s);
+	return false;
+}
+
+bool walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
+		 bool rice_s, hipStream_t s)
+{
+	const size_t lds = (size_t)(k.img_words + 4u) * 4u;
+	if (sample_bytes == 2)
+		return pre_p == PRE_DIFF ? walk_launch_p<2, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
+					 : walk_launch_p<2, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);
+	return pre_p == PRE_DIFF ? walk_launch_p<4, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
+				 : walk_launch_p<4, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);
+}
+
+} // namespace airs

@@ -453,65 +453,6 @@ __device__ __forceinline__ uint32_t be_pair(uint32_t s0, uint32_t s1)
 	return ((s0 >> 8) & 0xFFu) | ((s0 & 0xFFu) << 8) | (((s1 >> 8) & 0xFFu) << 16) | ((s1 & 0xFFu) << 24);
 }
 
-template <int W>
-__global__ __launch_bounds__(64) void checksum_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
-						       uint32_t num_frames, const uint32_t *frame_list,
-						       uint32_t *out)
-{
-	const uint32_t lf = blockIdx.x * 16u + (threadIdx.x >> 2);
-	const uint32_t q = threadIdx.x & 3u;
-	if (lf >= num_frames)
-		return;
-	const uint32_t frame = frame_list ? frame_list[lf] : lf;
-	const uint8_t *f = src + (uint64_t)frame * stride;
-	const uint32_t seed = 419764627u;
-	const uint32_t len = 2u * n;
-	const uint32_t stripes = len >= 16u ? n / 8u : 0u;
-	uint32_t acc = q == 0 ? seed + XP1 + XP2 : q == 1 ? seed + XP2 : q == 2 ? seed : seed - XP1;
-	// The accumulator chain is serial (xxhash round: acc = rotl(acc + x P2, 13) P1),
-	// so the loads of a batch of 16 stripes are issued before its 16 rounds and
-	// x P2 is computed off the chain: the chain is then add, rotate, multiply.
-	uint32_t s = 0;
-	if (W == 2 && ((uintptr_t)f & 3u) == 0) { // lane q's 4 bytes of a stripe are one aligned dword
-		const uint32_t *f32 = reinterpret_cast<const uint32_t *>(f);
-		for (; s + 16u <= stripes; s += 16u) {
-			uint32_t xv[16];
-#pragma unroll
-			for (uint32_t u = 0; u < 16u; u++)
-				xv[u] = __builtin_amdgcn_perm(f32[4u * (s + u) + q], f32[4u * (s + u) + q], 0x02030001u) * XP2;
-#pragma unroll
-			for (uint32_t u = 0; u < 16u; u++)
-				acc = rotl32(acc + xv[u], 13) * XP1;
-		}
-	}
-	for (; s < stripes; s++) {
-		const uint32_t i = 8u * s + 2u * q;
-		acc = rotl32(acc + be_pair(sample_at<W>(f, i), sample_at<W>(f, i + 1u)) * XP2, 13) * XP1;
-	}
-	// gather the four lanes into lane 0 of the quad
-	const uint32_t a1 = __shfl_down(acc, 1, 4), a2 = __shfl_down(acc, 2, 4), a3 = __shfl_down(acc, 3, 4);
-	if (q != 0)
-		return;
-	uint32_t h = stripes ? rotl32(acc, 1) + rotl32(a1, 7) + rotl32(a2, 12) + rotl32(a3, 18) : seed + XP5;
-	h += len;
-	uint32_t i = 8u * stripes; // next sample
-	const uint32_t rem_bytes = len - 16u * stripes;
-	uint32_t b = 0;
-	for (; b + 4u <= rem_bytes; b += 4u, i += 2u)
-		h = rotl32(h + be_pair(sample_at<W>(f, i), sample_at<W>(f, i + 1u)) * XP3, 17) * XP4;
-	if (b < rem_bytes) { // one sample (2 bytes) left
-		const uint32_t s0 = sample_at<W>(f, i);
-		h = rotl32(h + ((s0 >> 8) & 0xFFu) * XP5, 11) * XP1;
-		h = rotl32(h + (s0 & 0xFFu) * XP5, 11) * XP1;
-	}
-	h ^= h >> 15;
-	h *= XP2;
-	h ^= h >> 13;
-	h *= XP3;
-	h ^= h >> 16;
-	out[frame] = h;
-}
-
 // one XXH32 round with the input's P2 product already formed: add, rotate,
 // multiply as three dependent instructions (the compiler would fuse the add
 // into a 64-bit v_mad_u64_u32, whose latency is longer)
@@ -651,203 +592,6 @@ __global__ __launch_bounds__(64) void ck_chain_kernel(const uint8_t *src, uint64
 	out[frame] = h;
 }
 
-
-// The checksum bytes of an encode launch whose checksums ran on the second
-// stream (airs_dev_encode): the kernel's epilogue left each frame's payload
-// bytes in ck_at; the bytes that fit the capacity follow the payload, as the
-// epilogue stores them otherwise (reference cmp.c:386-390).
-__global__ __launch_bounds__(256) void ck_emit_kernel(uint8_t *dst, uint64_t dst_stride, uint32_t cap,
-						      uint32_t num_frames, const uint32_t *frame_list, uint32_t frame_add,
-						      uint32_t frame_mul, const uint32_t *ck_at, const uint32_t *checksums)
-{
-	const uint32_t lf = blockIdx.x * 256u + threadIdx.x;
-	if (lf >= num_frames)
-		return;
-	const uint32_t frame = frame_list ? frame_list[lf] : frame_add + lf * frame_mul;
-	if (frame == AIRS_NO_FRAME)
-		return;
-	const uint32_t pb = ck_at[lf], ck = checksums[frame];
-	uint8_t *fdst = dst + (uint64_t)frame * dst_stride;
-	for (uint32_t b = 0; b < 4u; b++)
-		if (pb + b < cap)
-			fdst[pb + b] = (uint8_t)(ck >> (24u - 8u * b));
-}
-
-// XXH32 with the accumulator chains split from their inputs: one consumer
-// wave runs the 64 serial chains of 16 frames (4 lanes per frame, as
-// checksum_kernel) and does only add, rotate, multiply per round; three
-// producer waves load the stripes, form the big-endian words and multiply
-// by P2 into a two-slot LDS ring, one slot ahead of the consumer.  A
-// round costs the chain wave 3 VALU instructions instead of 5 (two of
-// which were quarter-rate multiplies).  Frames of a block share n, so all
-// chains take the same number of rounds.
-#define CK_RS 256u // rounds per ring slot
-template <int W>
-__global__ __launch_bounds__(256) void checksum_pc_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
-							  uint32_t num_frames, const uint32_t *frame_list,
-							  uint32_t *out)
-{
-	// ring[slot][round / 4][chain] holds the inputs of rounds 4 rb .. 4 rb + 3
-	__shared__ uint4 ring[2][CK_RS / 4][64];
-	__shared__ uint64_t s_fbase[16];
-	const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-	const uint32_t nloc = min(16u, num_frames - blockIdx.x * 16u);
-	if (tid < 16u) {
-		const uint32_t lf = blockIdx.x * 16u + tid;
-		const uint32_t fr = tid < nloc ? (frame_list ? frame_list[lf] : lf) : 0u;
-		s_fbase[tid] = (uint64_t)(uintptr_t)(src + (uint64_t)fr * stride);
-	}
-	__syncthreads();
-	const uint32_t len = 2u * n;
-	const uint32_t stripes = len >= 16u ? n / 8u : 0u;
-	const uint32_t nslots = (stripes + CK_RS - 1u) / CK_RS;
-
-	// every load of a slot is issued before the first is used (22 stripes per
-	// producer thread in flight); unaligned frames take the per-sample path
-	constexpr uint32_t PER = (16u * CK_RS + 191u) / 192u;
-	constexpr uint32_t LPS = W == 2 ? 1u : 2u; // 16-byte loads per stripe
-#ifndef AIRS_CK_ABL // experiments: 1 producers idle, 2 consumer idle
-#define AIRS_CK_ABL 0
-#endif
-	auto produce = [&](uint32_t slot) {
-		if (AIRS_CK_ABL == 1)
-			return;
-		uint32_t *R = reinterpret_cast<uint32_t *>(&ring[slot & 1u][0][0]);
-		const uint32_t r0 = slot * CK_RS;
-		uint4 v[PER][LPS];
-#pragma unroll
-		for (uint32_t k = 0; k < PER; k++) {
-			const uint32_t it = tid - 64u + 192u * k;
-			const uint32_t fl = it / CK_RS, rr = it - fl * CK_RS, r = r0 + rr;
-			const uint8_t *f = reinterpret_cast<const uint8_t *>((uintptr_t)s_fbase[fl < 16u ? fl : 0u]);
-			if (it < 16u * CK_RS && fl < nloc && r < stripes && ((uintptr_t)f & 15u) == 0u) {
-				// from the kernel argument, so that the loads are global, not flat
-				const uint4 *g = reinterpret_cast<const uint4 *>(src + ((uintptr_t)f - (uintptr_t)src));
-#pragma unroll
-				for (uint32_t h = 0; h < LPS; h++)
-					v[k][h] = g[LPS * r + h];
-			}
-		}
-#pragma unroll
-		for (uint32_t k = 0; k < PER; k++) {
-			const uint32_t it = tid - 64u + 192u * k;
-			const uint32_t fl = it / CK_RS, rr = it - fl * CK_RS, r = r0 + rr;
-			if (it >= 16u * CK_RS || fl >= nloc || r >= stripes)
-				continue;
-			const uint8_t *f = reinterpret_cast<const uint8_t *>((uintptr_t)s_fbase[fl]);
-			uint32_t y[4];
-			if (((uintptr_t)f & 15u) == 0u) {
-				if (W == 2) {
-					y[0] = __builtin_amdgcn_perm(v[k][0].x, v[k][0].x, 0x02030001u);
-					y[1] = __builtin_amdgcn_perm(v[k][0].y, v[k][0].y, 0x02030001u);
-					y[2] = __builtin_amdgcn_perm(v[k][0].z, v[k][0].z, 0x02030001u);
-					y[3] = __builtin_amdgcn_perm(v[k][0].w, v[k][0].w, 0x02030001u);
-				} else {
-					y[0] = be_pair(v[k][0].x & 0xFFFFu, v[k][0].y & 0xFFFFu);
-					y[1] = be_pair(v[k][0].z & 0xFFFFu, v[k][0].w & 0xFFFFu);
-					y[2] = be_pair(v[k][LPS - 1].x & 0xFFFFu, v[k][LPS - 1].y & 0xFFFFu);
-					y[3] = be_pair(v[k][LPS - 1].z & 0xFFFFu, v[k][LPS - 1].w & 0xFFFFu);
-				}
-			} else {
-#pragma unroll
-				for (uint32_t qq = 0; qq < 4u; qq++)
-					y[qq] = be_pair(sample_at<W>(f, 8u * r + 2u * qq), sample_at<W>(f, 8u * r + 2u * qq + 1u));
-			}
-			// row rb = rr / 4, column chain ^ (rb mod 16): the 64 lanes of a
-			// store (64 consecutive rounds of one frame) hit 64 banks
-#pragma unroll
-			for (uint32_t qq = 0; qq < 4u; qq++)
-				R[((rr >> 2) * 64u + ((fl * 4u + qq) ^ ((rr >> 2) & 15u))) * 4u + (rr & 3u)] = y[qq] * XP2;
-		}
-	};
-
-	const uint32_t q = lane & 3u, fl = lane >> 2;
-	const uint32_t seed = 419764627u;
-	uint32_t acc = q == 0 ? seed + XP1 + XP2 : q == 1 ? seed + XP2 : q == 2 ? seed : seed - XP1;
-	if (wid != 0 && nslots)
-		produce(0);
-	__syncthreads();
-	for (uint32_t sl = 0; sl < nslots; sl++) {
-		if (wid == 0 && AIRS_CK_ABL != 2) {
-			const uint32_t nr = min(CK_RS, stripes - sl * CK_RS);
-			const uint4 *Rs = &ring[sl & 1u][0][0];
-			uint32_t rb = 0;
-			// 16 rounds per step, the next step's inputs read from LDS before
-			// this step's chain runs (the LDS latency stays off the chain)
-			if (16u <= nr) {
-				uint4 cur[4];
-#pragma unroll
-				for (uint32_t u = 0; u < 4u; u++)
-					cur[u] = Rs[u * 64u + (lane ^ u)];
-				for (; 4u * rb + 16u <= nr; rb += 4u) {
-					uint4 nxt[4];
-					// (past the slot's last step: a valid LDS row, value unused)
-#pragma unroll
-					for (uint32_t u = 0; u < 4u; u++)
-						{
-						const uint32_t row = min(rb + 4u + u, CK_RS / 4u - 1u);
-						nxt[u] = Rs[row * 64u + (lane ^ (row & 15u))];
-					}
-#pragma unroll
-					for (uint32_t u = 0; u < 4u; u++) {
-						acc = xxh_round_pre(acc, cur[u].x);
-						acc = xxh_round_pre(acc, cur[u].y);
-						acc = xxh_round_pre(acc, cur[u].z);
-						acc = xxh_round_pre(acc, cur[u].w);
-					}
-#pragma unroll
-					for (uint32_t u = 0; u < 4u; u++)
-						cur[u] = nxt[u];
-				}
-			}
-			for (; 4u * rb + 4u <= nr; rb++) {
-				const uint4 v = Rs[rb * 64u + (lane ^ (rb & 15u))];
-				acc = xxh_round_pre(acc, v.x);
-				acc = xxh_round_pre(acc, v.y);
-				acc = xxh_round_pre(acc, v.z);
-				acc = xxh_round_pre(acc, v.w);
-			}
-			if (4u * rb < nr) {
-				const uint4 v = Rs[rb * 64u + (lane ^ (rb & 15u))];
-				const uint32_t left = nr - 4u * rb;
-				acc = xxh_round_pre(acc, v.x);
-				if (left > 1u)
-					acc = xxh_round_pre(acc, v.y);
-				if (left > 2u)
-					acc = xxh_round_pre(acc, v.z);
-			}
-		} else if (sl + 1u < nslots) {
-			produce(sl + 1u);
-		}
-		__syncthreads();
-	}
-	if (wid != 0 || fl >= nloc)
-		return;
-	// tail of the frame: as checksum_kernel
-	const uint8_t *f = reinterpret_cast<const uint8_t *>((uintptr_t)s_fbase[fl]);
-	const uint32_t a1 = __shfl_down(acc, 1, 4), a2 = __shfl_down(acc, 2, 4), a3 = __shfl_down(acc, 3, 4);
-	if (q != 0)
-		return;
-	uint32_t h = stripes ? rotl32(acc, 1) + rotl32(a1, 7) + rotl32(a2, 12) + rotl32(a3, 18) : seed + XP5;
-	h += len;
-	uint32_t i = 8u * stripes;
-	const uint32_t rem_bytes = len - 16u * stripes;
-	uint32_t b = 0;
-	for (; b + 4u <= rem_bytes; b += 4u, i += 2u)
-		h = rotl32(h + be_pair(sample_at<W>(f, i), sample_at<W>(f, i + 1u)) * XP3, 17) * XP4;
-	if (b < rem_bytes) {
-		const uint32_t s0 = sample_at<W>(f, i);
-		h = rotl32(h + ((s0 >> 8) & 0xFFu) * XP5, 11) * XP1;
-		h = rotl32(h + (s0 & 0xFFu) * XP5, 11) * XP1;
-	}
-	h ^= h >> 15;
-	h *= XP2;
-	h ^= h >> 13;
-	h *= XP3;
-	h ^= h >> 16;
-	const uint32_t lfg = blockIdx.x * 16u + fl;
-	out[frame_list ? frame_list[lfg] : lfg] = h;
-}
 
 // ---------------------------------------------------------------------
 // Per-frame Rice parameter selection (build-defined rule; oracle
@@ -1102,8 +846,10 @@ __global__ __launch_bounds__(256) void pack_copy_kernel(const uint8_t *src, uint
 	const uint32_t nw = (sz + 7u) >> 3; // 8-byte words of the frame
 	const uint2 *s8 = reinterpret_cast<const uint2 *>(src + (uint64_t)f * stride);
 	uint2 *o8 = reinterpret_cast<uint2 *>(out + offsets[f]);
-	for (uint32_t j = blockIdx.y * 1024u + threadIdx.x; j < nw && j < (blockIdx.y + 1u) * 1024u; j += 256u)
-		o8[j] = s8[j];
+	// blocks of 1024 words, grid-stride over y (gridDim.y is capped at 65535)
+	for (uint32_t b = blockIdx.y; (uint64_t)b * 1024u < nw; b += gridDim.y)
+		for (uint32_t j = b * 1024u + threadIdx.x; j < nw && j < (b + 1u) * 1024u; j += 256u)
+			o8[j] = s8[j];
 }
 
 // identifier patch after fallback resolution (header bytes 8..13)
@@ -1166,6 +912,19 @@ using namespace airs;
 
 static thread_local char g_err[256];
 
+#if AIRS_ABLATE
+// Ablation builds only (scripts/build_exp.sh -DAIRS_ABLATE=1): the AIRS_DBG
+// switches of enc_common.h DBG(), set by the benchmark harness
+// (scripts/kbench.py) through this entry point; the product build has none.
+static uint32_t g_dbg;
+static char g_dbgts_path[512];
+extern "C" void airs_dev_set_debug(uint32_t bits, const char *timeline_path)
+{
+	g_dbg = bits;
+	snprintf(g_dbgts_path, sizeof(g_dbgts_path), "%s", timeline_path ? timeline_path : "");
+}
+#endif
+
 static uint32_t hip_fail(hipError_t e, const char *what)
 {
 	snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
@@ -1194,22 +953,7 @@ struct airs_dev_engine {
 	size_t dbgts_n;
 	uint64_t *ktot; // fused Rice selection: 16 candidate granules per segment
 	size_t ktot_cap;
-	// checksums run on a second stream, overlapped with the encode
-	// (airs_dev_checksum); ck_pending = the output of the one not yet joined
-	hipStream_t ck_stream;
-	hipEvent_t ck_ready, ck_done;
-	const uint32_t *ck_pending;
 };
-
-// the main stream waits for the pending checksum (every consumer of the
-// checksums, or of the main stream's results, comes after this)
-static void ck_join(airs_dev_engine *e)
-{
-	if (e->ck_pending) {
-		(void)hipStreamWaitEvent(e->stream, e->ck_done, 0);
-		e->ck_pending = nullptr;
-	}
-}
 
 extern "C" int airs_dev_available(void)
 {
@@ -1239,14 +983,6 @@ extern "C" struct airs_dev_engine *airs_dev_engine_create(void *stream)
 		return nullptr;
 	}
 	e->epoch = 0;
-	if (hipStreamCreateWithFlags(&e->ck_stream, hipStreamNonBlocking) != hipSuccess ||
-	    hipEventCreateWithFlags(&e->ck_ready, hipEventDisableTiming) != hipSuccess ||
-	    hipEventCreateWithFlags(&e->ck_done, hipEventDisableTiming) != hipSuccess) {
-		snprintf(g_err, sizeof(g_err), "stream/event creation failed");
-		(void)hipFree(e->ticket);
-		free(e);
-		return nullptr;
-	}
 	return e;
 }
 
@@ -1254,12 +990,7 @@ extern "C" void airs_dev_engine_destroy(struct airs_dev_engine *e)
 {
 	if (!e)
 		return;
-	ck_join(e);
 	(void)hipStreamSynchronize(e->stream);
-	(void)hipStreamSynchronize(e->ck_stream);
-	(void)hipEventDestroy(e->ck_ready);
-	(void)hipEventDestroy(e->ck_done);
-	(void)hipStreamDestroy(e->ck_stream);
 	(void)hipFree(e->agg);
 	(void)hipFree(e->tail);
 	(void)hipFree(e->ticket);
@@ -1281,7 +1012,6 @@ extern "C" void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t by
 		return nullptr;
 	if (e->scratch_cap[slot] < bytes) {
 		(void)hipStreamSynchronize(e->stream);
-		(void)hipStreamSynchronize(e->ck_stream);
 		(void)hipFree(e->scratch[slot]);
 		e->scratch[slot] = nullptr;
 		e->scratch_cap[slot] = 0;
@@ -1349,36 +1079,31 @@ template <int W, int PRE, int ENC, bool RICE, int MODEL>
 static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t s)
 {
 	if constexpr (ENC == ENC_ZERO && RICE && MODEL == 0 && (PRE == PRE_NONE || PRE == PRE_DIFF)) {
-		if (k.ktot) { // fused per-frame Rice selection
+		if (k.ktot) { // fused per-frame Rice selection (frame barrier: never persistent)
 			size_t lds = (size_t)2u * (k.img_words + 4u) * 4u; // two images (enc_kernel.h NIMG)
 			lds = lds > AUTO_BINS * 64u * 4u ? lds : AUTO_BINS * 64u * 4u; // the histogram
 			if (full)
-				hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true, true>), dim3(grid),
-						   dim3(EWG), lds, s, k);
+				launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, true, true>, k, grid, lds, s, false);
 			else
-				hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, false, true>), dim3(grid),
-						   dim3(EWG), lds, s, k);
+				launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, false, true>, k, grid, lds, s, false);
 			return;
 		}
 	}
-#ifndef AIRS_LDS_EXTRA
-#define AIRS_LDS_EXTRA 0
-#endif
-	const size_t lds = (size_t)seg_images(W, MODEL) * (k.img_words + 4u) * 4u + AIRS_LDS_EXTRA; // (extra: occupancy experiments)
+	const size_t lds = (size_t)seg_images(W, MODEL) * (k.img_words + 4u) * 4u;
 #ifdef AIRS_EXP_ONLY
 	// experiment builds: only the benchmark kernels (u16/i16, DIFF, ZERO, Rice, FULL)
 	if constexpr (!(W == 2 && PRE == PRE_DIFF && ENC == ENC_ZERO && RICE && MODEL == 0)) {
 		return;
 	} else {
 		if (full)
-			hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true>), dim3(grid), dim3(EWG), lds, s, k);
+			launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, true>, k, grid, lds, s, true);
 		return;
 	}
 #else
 	if (full)
-		hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, true>), dim3(grid), dim3(EWG), lds, s, k);
+		launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, true>, k, grid, lds, s, true);
 	else
-		hipLaunchKernelGGL((encode_kernel<W, PRE, ENC, RICE, MODEL, false>), dim3(grid), dim3(EWG), lds, s, k);
+		launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, false>, k, grid, lds, s, true);
 #endif
 }
 
@@ -1531,20 +1256,7 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 		return ERRV(E_PARAMS_INVALID);
 	if (L->encoder_type > ENC_MULTI || (L->sample_bytes != 2 && L->sample_bytes != 4))
 		return ERRV(E_PARAMS_INVALID);
-	// the persistent pipelined kernel (enc_pipe.hip) takes whole segments of
-	// 16-byte aligned frames without a model.  Experimental: AIRS_PIPE=1
-	// selects it (see DESIGN.md for its measurements)
-	static int pipe_env = -1;
-	if (pipe_env < 0) {
-		const char *v = getenv("AIRS_PIPE");
-		pipe_env = v ? atoi(v) : 0;
-	}
-	const bool pipe = pipe_env != 0 && !L->auto_rice && L->model_mode == AIRS_MODEL_NONE &&
-			  (L->preprocessing == PRE_NONE || L->preprocessing == PRE_DIFF) &&
-			  L->n % pipe_segn(L->sample_bytes) == 0u &&
-			  ((uintptr_t)L->src & 15u) == 0u && (L->src_stride & 15u) == 0u;
-	const uint32_t segn =
-		pipe ? pipe_segn(L->sample_bytes) : seg_chunks(L->sample_bytes == 4 ? 4 : 2, L->model_mode ? 1 : 0) * AIRS_SEG;
+	const uint32_t segn = seg_chunks(L->sample_bytes == 4 ? 4 : 2, L->model_mode ? 1 : 0) * AIRS_SEG;
 	const uint32_t spf = (L->n + segn - 1) / segn;
 	const uint64_t segs = (uint64_t)spf * L->num_frames;
 	if (segs > 0x7FFFFFFFull)
@@ -1552,19 +1264,9 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	uint32_t r = ensure_granules(e, (size_t)segs);
 	if (r)
 		return r;
-	// checksums still running on the second stream: this launch leaves their
-	// bytes to ck_emit_kernel and overlaps them; anything else waits for them
-	uint32_t *ck_at = nullptr;
-	if (e->ck_pending && L->checksum_enabled && L->checksums == e->ck_pending && !pipe) {
-		ck_at = (uint32_t *)airs_dev_scratch(e, AIRS_NSLOT - 5, (size_t)L->num_frames * 4u);
-		if (!ck_at)
-			return ERRV(E_GENERIC);
-	} else {
-		ck_join(e);
-	}
 	// CMP_GPU_AUTO_RICE: fused into the encode kernel for frames of a few
 	// segments without a model; otherwise select_rice_kernel writes g first
-	const bool auto_fused = L->auto_rice && !pipe && L->encoder_type == ENC_ZERO &&
+	const bool auto_fused = L->auto_rice && L->encoder_type == ENC_ZERO &&
 				L->model_mode == AIRS_MODEL_NONE &&
 				(L->preprocessing == PRE_NONE || L->preprocessing == PRE_DIFF) && spf <= AUTO_MAX_SPF;
 	const uint32_t *frame_g = L->frame_g;
@@ -1600,7 +1302,6 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	k.ktot = auto_fused ? e->ktot : nullptr;
 	k.seqs = L->seqs;
 	k.checksums = L->checksums;
-	k.ck_at = ck_at;
 	k.ids = L->ids;
 	k.status = L->status;
 	k.needed = L->needed;
@@ -1633,24 +1334,19 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	k.ticket_base = e->ticket_base;
 	k.img_words = image_words(L->encoder_type, (frame_g || auto_fused) ? 0u : L->encoder_param);
 	k.epoch = next_epoch(e);
-	{
-		static int dbg = -1;
-		if (dbg < 0) {
-			const char *v = getenv("AIRS_DBG");
-			dbg = v ? atoi(v) : 0;
+#if AIRS_ABLATE
+	k.dbg = g_dbg;
+	if (g_dbg & 65536) {
+		if (e->dbgts_n < 8u * segs) {
+			(void)hipFree(e->dbgts);
+			e->dbgts_n = 8u * segs;
+			if (hipMalloc(&e->dbgts, e->dbgts_n * 8u) != hipSuccess)
+				return ERRV(E_GENERIC);
 		}
-		k.dbg = (uint32_t)dbg;
-		if (dbg & 65536) {
-			if (e->dbgts_n < 8u * segs) {
-				(void)hipFree(e->dbgts);
-				e->dbgts_n = 8u * segs;
-				if (hipMalloc(&e->dbgts, e->dbgts_n * 8u) != hipSuccess)
-					return ERRV(E_GENERIC);
-			}
-			HIPCHECK(hipMemsetAsync(e->dbgts, 0, 8u * segs * 8u, e->stream));
-			k.dbgts = e->dbgts;
-		}
+		HIPCHECK(hipMemsetAsync(e->dbgts, 0, 8u * segs * 8u, e->stream));
+		k.dbgts = e->dbgts;
 	}
+#endif
 
 	bool rice = frame_g != nullptr || auto_fused ||
 		    (L->encoder_param && (L->encoder_param & (L->encoder_param - 1u)) == 0u);
@@ -1670,11 +1366,7 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	// LBC): only when no frame can stop early (no fail bit)
 	if (L->model_mode != AIRS_MODEL_NONE)
 		full = full && L->fail_bit == UINT64_MAX;
-	if (pipe) {
-		r = pipe_encode(k, L->sample_bytes, L->preprocessing, L->encoder_type, rice, e->stream);
-		if (r)
-			return r;
-	} else {
+	{
 		// fused Rice selection: whole groups of 8 frames (XCD-local frames)
 		const uint32_t grid = auto_fused ? (L->num_frames + 7u) / 8u * 8u * spf : (uint32_t)segs;
 		if (L->sample_bytes == 2)
@@ -1683,15 +1375,81 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 			dispatch_pre<4>(k, L->preprocessing, L->encoder_type, rice, full, L->model_mode, grid, e->stream);
 	}
 	HIPCHECK(hipGetLastError());
-	if (ck_at) {
-		ck_join(e);
-		hipLaunchKernelGGL(ck_emit_kernel, dim3((L->num_frames + 255u) / 256u), dim3(256), 0, e->stream, k.dst,
-				   k.dst_stride, k.cap, L->num_frames, k.frame_list, k.frame_add, k.frame_mul, ck_at,
-				   k.checksums);
-		HIPCHECK(hipGetLastError());
-	}
 	if (k.dbg & 4u)
 		e->ticket_base += (uint32_t)segs;
+	return 0;
+}
+
+// ---- MODEL streams in one launch (enc_walk.hip) ----------------------------
+static bool walk_rice(uint32_t enc, uint32_t g)
+{
+	return (enc == ENC_ZERO || enc == ENC_MULTI) && g && (g & (g - 1u)) == 0u;
+}
+
+extern "C" int airs_dev_walk_supported(const struct airs_walk *w)
+{
+	if (!w || !w->n || w->n % AIRS_SEG || !w->num_ctx || !w->fpc || (w->sample_bytes != 2 && w->sample_bytes != 4))
+		return 0;
+	if ((w->pre_p != PRE_NONE && w->pre_p != PRE_DIFF) || !walk_rice(w->enc_p, w->g_p) ||
+	    !walk_rice(w->enc_s, w->g_s) || w->model_rate > 16u)
+		return 0;
+	if (((uintptr_t)w->src & 15u) || (w->src_stride & 15u))
+		return 0;
+	if (!w->model_ptrs && (((uintptr_t)w->model & 15u) || (w->model_stride & 15u)))
+		return 0;
+	const uint64_t segs = (uint64_t)w->num_ctx * (w->n / AIRS_SEG);
+	return segs <= 0x7FFFFFFFull && segs * w->fpc <= 0x7FFFFFFFull;
+}
+
+extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_walk *w)
+{
+	if (!e || !airs_dev_walk_supported(w))
+		return ERRV(E_PARAMS_INVALID);
+	const uint32_t spf = w->n / AIRS_SEG;
+	const uint64_t total = (uint64_t)w->num_ctx * w->fpc;
+	uint32_t r = ensure_granules(e, (size_t)(total * spf));
+	if (r)
+		return r;
+	WArgs k;
+	memset(&k, 0, sizeof(k));
+	k.src = (const uint8_t *)w->src;
+	k.src_stride = w->src_stride;
+	k.dst = (uint8_t *)w->dst;
+	k.dst_stride = w->dst_stride;
+	k.cap = w->cap;
+	k.model = (uint8_t *)w->model;
+	k.model_stride = w->model_stride;
+	k.model_ptrs = w->model_ptrs;
+	k.checksums = w->checksums;
+	k.checksum = w->checksum_enabled ? 1u : 0u;
+	k.ids = w->ids;
+	k.id_base = w->id_base;
+	k.id_cstep = w->id_cstep;
+	k.id_astep = w->id_astep;
+	k.seq0s = w->seq0s;
+	k.seq0 = w->seq0;
+	k.status = w->status;
+	k.agg = e->agg;
+	k.tail = e->tail;
+	k.ticket = e->ticket;
+	k.n = w->n;
+	k.spf = spf;
+	k.num_ctx = w->num_ctx;
+	k.fpc = w->fpc;
+	k.iters = w->iters;
+	k.g_p = w->g_p;
+	k.outl_p = w->outl_p;
+	k.g_s = w->g_s;
+	k.outl_s = w->outl_s;
+	k.model_rate = w->model_rate;
+	k.is_unsigned = w->is_unsigned;
+	// one image for the longer-coded of the two passes (plus a flush word)
+	const uint32_t iw_p = image_words(w->enc_p, w->g_p), iw_s = image_words(w->enc_s, w->g_s);
+	k.img_words = (iw_p > iw_s ? iw_p : iw_s) + 4u;
+	k.epoch = next_epoch(e);
+	if (!walk_encode(k, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream))
+		return ERRV(E_PARAMS_INVALID);
+	HIPCHECK(hipGetLastError());
 	return 0;
 }
 
@@ -1744,70 +1502,29 @@ extern "C" uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src
 	if (!e || !n || !num_frames)
 		return ERRV(E_GENERIC);
 	dim3 grid((num_frames + 15) / 16);
-	// two launches (ck_pre + ck_chain) by default;
-	// AIRS_CK_ALG=1: the single-wave kernel, 2: the producer/consumer kernel
-	static int alg = -1;
-	if (alg < 0) {
-		const char *v = getenv("AIRS_CK_ALG");
-		alg = v ? atoi(v) : 0;
-	}
+	// two launches: ck_pre_kernel forms the stripes' x P2
+	// products, ck_chain_kernel runs the serial accumulator chains
 	const uint32_t stripes = 2u * n >= 16u ? n / 8u : 0u;
-	// AIRS_CK_OVERLAP=1: the chains on a second stream, overlapped with the
-	// next encode launch.  Measured slower (the chain wave,
-	// issue-bound, loses ~8 % beside the encode even on a CU of its own),
-	// so both launches stay on the main stream by default
-	static int overlap = -1;
-	if (overlap < 0) {
-		const char *v = getenv("AIRS_CK_OVERLAP");
-		overlap = v ? atoi(v) : 0;
-	}
-	ck_join(e);
-	if (alg == 0 && stripes) {
-		const uint32_t S4 = (stripes + 3u) & ~3u;
-		// whole groups of 16 frames x 4 chains
-		uint32_t *Y = (uint32_t *)airs_dev_scratch(e, AIRS_NSLOT - 4, (size_t)grid.x * 64u * S4 * 4u);
-		if (!Y)
-			return ERRV(E_GENERIC);
+	const uint32_t S4 = (stripes + 3u) & ~3u;
+	// whole groups of 16 frames x 4 chains
+	uint32_t *Y = (uint32_t *)airs_dev_scratch(e, AIRS_NSLOT - 4, (size_t)grid.x * 64u * S4 * 4u);
+	if (!Y)
+		return ERRV(E_GENERIC);
+	if (stripes) {
 		const dim3 pg(grid.x, min((S4 / 4u + 15u) / 16u, 65535u));
-		// the products on the main stream; the chains there too, or on the
-		// second stream (AIRS_CK_OVERLAP=1)
 		if (sample_bytes == 2)
 			hipLaunchKernelGGL(ck_pre_kernel<2>, pg, dim3(256), 0, e->stream, (const uint8_t *)src, src_stride,
 					   n, num_frames, frame_list, S4, Y);
 		else
 			hipLaunchKernelGGL(ck_pre_kernel<4>, pg, dim3(256), 0, e->stream, (const uint8_t *)src, src_stride,
 					   n, num_frames, frame_list, S4, Y);
-		hipStream_t cs = e->stream;
-		if (overlap) {
-			HIPCHECK(hipEventRecord(e->ck_ready, e->stream));
-			HIPCHECK(hipStreamWaitEvent(e->ck_stream, e->ck_ready, 0));
-			cs = e->ck_stream;
-		}
-		if (sample_bytes == 2)
-			hipLaunchKernelGGL(ck_chain_kernel<2>, grid, dim3(64), 0, cs, (const uint8_t *)src, src_stride, n,
-					   num_frames, frame_list, S4, (const uint32_t *)Y, out);
-		else
-			hipLaunchKernelGGL(ck_chain_kernel<4>, grid, dim3(64), 0, cs, (const uint8_t *)src, src_stride, n,
-					   num_frames, frame_list, S4, (const uint32_t *)Y, out);
-		HIPCHECK(hipGetLastError());
-		if (overlap) {
-			HIPCHECK(hipEventRecord(e->ck_done, e->ck_stream));
-			e->ck_pending = out;
-		}
-	} else if (alg != 2) {
-		if (sample_bytes == 2)
-			hipLaunchKernelGGL(checksum_kernel<2>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
-					   src_stride, n, num_frames, frame_list, out);
-		else
-			hipLaunchKernelGGL(checksum_kernel<4>, grid, dim3(64), 0, e->stream, (const uint8_t *)src,
-					   src_stride, n, num_frames, frame_list, out);
-	} else if (sample_bytes == 2) {
-		hipLaunchKernelGGL(checksum_pc_kernel<2>, grid, dim3(256), 0, e->stream, (const uint8_t *)src,
-				   src_stride, n, num_frames, frame_list, out);
-	} else {
-		hipLaunchKernelGGL(checksum_pc_kernel<4>, grid, dim3(256), 0, e->stream, (const uint8_t *)src,
-				   src_stride, n, num_frames, frame_list, out);
 	}
+	if (sample_bytes == 2)
+		hipLaunchKernelGGL(ck_chain_kernel<2>, grid, dim3(64), 0, e->stream, (const uint8_t *)src, src_stride, n,
+				   num_frames, frame_list, S4, (const uint32_t *)Y, out);
+	else
+		hipLaunchKernelGGL(ck_chain_kernel<4>, grid, dim3(64), 0, e->stream, (const uint8_t *)src, src_stride, n,
+				   num_frames, frame_list, S4, (const uint32_t *)Y, out);
 	HIPCHECK(hipGetLastError());
 	return 0;
 }
@@ -1851,7 +1568,10 @@ extern "C" uint32_t airs_dev_fb_copy(struct airs_dev_engine *e, const struct air
 {
 	if (!e || !s || !s->num_ctx || s->prev < 0 || !s->n)
 		return ERRV(E_GENERIC);
-	ck_join(e); // the fallback frames carry the checksum
+	// frames of the device exact mode passed the prologue's size checks
+	// (2n <= 2^24 - 1, cmp_header.h), so y <= 4096 here
+	if ((s->n + 2047u) / 2048u > 65535u)
+		return ERRV(E_GENERIC);
 	const dim3 grid(s->num_ctx, (s->n + 2047u) / 2048u);
 	if (s->sample_bytes == 2)
 		hipLaunchKernelGGL(fb_copy_kernel<2>, grid, dim3(256), 0, e->stream, *s);
@@ -1869,7 +1589,7 @@ extern "C" uint32_t airs_dev_pack_frames(struct airs_dev_engine *e, const void *
 	    ((uintptr_t)out & 7u))
 		return ERRV(E_GENERIC);
 	hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(1024), 0, e->stream, sizes, num_frames, err_floor, offsets);
-	const uint32_t ny = (((uint64_t)max_frame_bytes + 7u) / 8u + 1023u) / 1024u;
+	const uint32_t ny = (uint32_t)min((((uint64_t)max_frame_bytes + 7u) / 8u + 1023u) / 1024u, (uint64_t)65535u);
 	hipLaunchKernelGGL(pack_copy_kernel, dim3(num_frames, ny ? ny : 1u), dim3(256), 0, e->stream,
 			   (const uint8_t *)src, src_stride, sizes, err_floor, offsets, (uint8_t *)out);
 	HIPCHECK(hipGetLastError());
@@ -1934,7 +1654,6 @@ extern "C" uint32_t airs_dev_d2h(struct airs_dev_engine *e, void *dst, const voi
 {
 	if (!bytes)
 		return 0;
-	ck_join(e);
 	HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream));
 	return 0;
 }
@@ -1950,35 +1669,28 @@ extern "C" uint32_t airs_dev_memset(struct airs_dev_engine *e, void *dst, int v,
 extern "C" uint32_t airs_dev_sync(struct airs_dev_engine *e)
 {
 	uint32_t faults = 0;
-	ck_join(e);
 	HIPCHECK(hipStreamSynchronize(e->stream));
 	HIPCHECK(hipMemcpy(&faults, e->ticket + AIRS_FAULT_WORD, sizeof(faults), hipMemcpyDeviceToHost));
-	{
-		static int dbg = -1;
-		if (dbg < 0) {
-			const char *v = getenv("AIRS_DBG");
-			dbg = v ? atoi(v) : 0;
+#if AIRS_ABLATE
+	if ((g_dbg & 65536) && g_dbgts_path[0]) { // the debug timeline (scripts/ts_analyze.py)
+		FILE *f = fopen(g_dbgts_path, "wb");
+		if (f && e->dbgts) {
+			uint64_t *h = (uint64_t *)malloc(e->dbgts_n * 8u);
+			if (h && hipMemcpy(h, e->dbgts, e->dbgts_n * 8u, hipMemcpyDeviceToHost) == hipSuccess)
+				fwrite(h, 8u, e->dbgts_n, f);
+			free(h);
 		}
-		if (dbg & 65536) { // dump the debug timeline to $AIRS_DBGTS_PATH
-			const char *path = getenv("AIRS_DBGTS_PATH");
-			FILE *f = path ? fopen(path, "wb") : nullptr;
-			if (f && e->dbgts) {
-				uint64_t *h = (uint64_t *)malloc(e->dbgts_n * 8u);
-				if (h && hipMemcpy(h, e->dbgts, e->dbgts_n * 8u, hipMemcpyDeviceToHost) == hipSuccess)
-					fwrite(h, 8u, e->dbgts_n, f);
-				free(h);
-			}
-			if (f)
-				fclose(f);
-		}
-		if (dbg & 256) {
-			uint32_t st[4];
-			HIPCHECK(hipMemcpy(st, e->ticket + 20, sizeof(st), hipMemcpyDeviceToHost));
-			fprintf(stderr, "airscmp look-back stats: lookbacks=%u rounds=%u retries=%u tail_repolls=%u\n", st[0],
-				st[1], st[2], st[3]);
-			(void)hipMemset(e->ticket + 20, 0, sizeof(st));
-		}
+		if (f)
+			fclose(f);
 	}
+	if (g_dbg & 256) {
+		uint32_t st[4];
+		HIPCHECK(hipMemcpy(st, e->ticket + 20, sizeof(st), hipMemcpyDeviceToHost));
+		fprintf(stderr, "airscmp look-back stats: lookbacks=%u rounds=%u retries=%u tail_repolls=%u\n", st[0],
+			st[1], st[2], st[3]);
+		(void)hipMemset(e->ticket + 20, 0, sizeof(st));
+	}
+#endif
 	if (faults) {
 		snprintf(g_err, sizeof(g_err), "%u look-back give-ups", faults);
 		fprintf(stderr, "airscmp: internal error: %s\n", g_err);

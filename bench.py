@@ -82,7 +82,7 @@ WORKLOADS = {
     "cfg5": dict(desc="configs[4]: 256 streams x 16 acquisitions x 64 Ki i16-in-i32 samples (256 Mi), "
                       "primary DIFF + GOLOMB_ZERO g=16, secondary MODEL + GOLOMB_MULTI g=8 o=107 rate=11",
                  kind="i16_in_i32", n=64 << 10, nctx=256, fpc=16, seed=0xA1A9, W=32, golden="cfg5_model",
-                 layout="block",
+                 layout="streams",
                  params=dict(primary_preprocessing=DIFF, primary_encoder_type=ZERO, primary_encoder_param=16,
                              secondary_iterations=15, secondary_preprocessing=MODEL,
                              secondary_encoder_type=MULTI, secondary_encoder_param=8,
@@ -128,9 +128,12 @@ def measured_traffic(wname):
 
 
 def frame_ids(wl, rank, world):
-    nf = wl["nctx"] * wl["fpc"]
+    """global frame numbers of this rank's frames, in local order (shard.py layouts)"""
+    nf, fpc = wl["nctx"] * wl["fpc"], wl["fpc"]
     if wl["layout"] == "roundrobin":
         return [rank + world * j for j in range(nf)]
+    if wl["layout"] == "streams":  # stream s on rank s mod N (its model stays on one GPU)
+        return [(rank + world * i) * fpc + a for i in range(wl["nctx"]) for a in range(fpc)]
     return [rank * nf + j for j in range(nf)]
 
 
@@ -301,7 +304,7 @@ class BufferSet:
         nf = self.nctx * self.fpc
         self.stride = n * sb
         self.src = torch.empty(nf * self.stride, dtype=torch.uint8, device="cuda")
-        if wl["W"] == "pow2_mod12" or wl["layout"] == "roundrobin":
+        if wl["W"] == "pow2_mod12" or fids != list(range(fids[0], fids[0] + nf)):
             for j, f in enumerate(fids):
                 assert eng.synthesize(self.src.data_ptr() + j * self.stride, sb, wl["seed"], f, n, 1, self.stride,
                                       noise_w(wl, f)) == 0
@@ -370,8 +373,9 @@ def main():
 
     wname = args.workload or ("cfg2" if world == 1 else "cfg4")
     wl = WORKLOADS[wname]
-    if world > 1 and wl["layout"] != "roundrobin":
-        raise SystemExit(f"--workload {wname} is a single-GPU config; N > 1 runs cfg4 (round-robin frames)")
+    if world > 1 and wl["layout"] not in ("roundrobin", "streams"):
+        raise SystemExit(f"--workload {wname} is a single-GPU config; N > 1 runs cfg4 (round-robin frames) or "
+                         f"cfg5 (streams)")
     n, nctx, fpc = wl["n"], wl["nctx"], wl["fpc"]
     nf = nctx * fpc
     sb = sample_bytes(wl)
@@ -385,6 +389,8 @@ def main():
         sets.append(BufferSet(torch, pkg, lib, eng, wl, fids))
     torch.cuda.synchronize()
 
+    draws = np.zeros(nf, dtype=np.uint8)  # identifier draws per frame (cmp_gpu_batch.draws), for the gather
+
     def step(bs):
         if wl.get("stream"):  # one payload-only stream over all the samples of the set
             p = wl["params"]
@@ -395,7 +401,7 @@ def main():
                 raise RuntimeError("cmp_gpu_encode_stream: " + api.error_name(r))
             return
         r = eng.compress(bs.ctxs, fpc, wl["kind"], bs.src.data_ptr(), bs.stride, bs.stride, bs.dst.data_ptr(),
-                         bs.dstride, bs.cap, bs.sizes.data_ptr(), flags)
+                         bs.dstride, bs.cap, bs.sizes.data_ptr(), flags, draws.ctypes.data)
         if r:
             raise RuntimeError("cmp_gpu_compress: " + api.error_name(r))
 
@@ -438,7 +444,7 @@ def main():
     key = f"shard_digests_n{world}" if wl["layout"] == "roundrobin" else None
     if key and key in gold:
         want = gold[key][rank]
-    elif wl["layout"] == "block" and rank == 0:
+    elif wl["layout"] in ("block", "streams") and world == 1:
         want = gold["sha256"] if wl.get("stream") else gold["digest"]
     else:
         want = None
@@ -473,17 +479,22 @@ def main():
     gather = None
     if world > 1 and not args.no_gather:
         bs = sets[0]
+        # identifiers of one process over the node's frames with the default
+        # counter (first draw 0): one context per stream, initialised in
+        # stream order, so the frame draws start after nctx_total - 1
+        nstreams = world * nctx if wl["layout"] == "streams" else 1
         gather, g = pkg.shard.gather_frames_timed(dist, bs.dst, bs.dstride, bs.sizes, nf, rank, world,
-                                                  layout="roundrobin", patch_base=0,
-                                                  params=api.CmpParams(**wl["params"]), engine=eng,
-                                                  frame_capacity=bs.cap)
+                                                  layout=wl["layout"], patch_base=nstreams - 1, engine=eng,
+                                                  frame_capacity=bs.cap, draws=draws, fpc=fpc)
         if g is not None:
             host_all = g.data.cpu().numpy()
-            offs, lens = g.offsets.numpy(), g.sizes.numpy()
+            offs, lens = g.offsets.cpu().numpy(), g.sizes.numpy()
             hg = hashlib.sha256()
             for f in range(g.num_frames):
                 b = bytearray(host_all[offs[f]:offs[f] + lens[f]])
-                ok_id = int.from_bytes(b[8:14], "big") == 1 + f
+                # cfg4: one draw per frame; cfg5: one per stream (its primary frame)
+                want_id = 1 + f if wl["layout"] != "streams" else nstreams + f // fpc
+                ok_id = int.from_bytes(b[8:14], "big") == want_id
                 b[8:14] = b"\0" * 6
                 hg.update(b)
                 if not ok_id:
@@ -507,8 +518,8 @@ def main():
         "cfg3": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO> (the per-frame Rice k chosen in-kernel): one "
                 "launch per step",
         "cfg4": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL>: one launch per step",
-        "cfg5": "encode_kernel<4,DIFF,ZERO,Rice,STORE> + 15 x encode_kernel<4,MODEL,MULTI,Rice,UPDATE>: 16 "
-                "launches per step (one per acquisition)",
+        "cfg5": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice> (enc_walk.hip): ONE launch per step, every "
+                "acquisition of the 256 streams, the models kept on the chip",
         "cfg5fb": "per acquisition: fb_step_kernel + fb_copy_kernel + encode_kernel<4,DIFF,ZERO,Rice,STORE> + "
                   "encode_kernel<4,MODEL,MULTI,Rice,UPDATE> (frame-list holes)",
     }
@@ -543,7 +554,8 @@ def main():
                 "sample_type": wl["kind"],
                 "params": wl["params"],
                 "auto_rice": bool(wl.get("auto_rice")),
-                "parallelism": f"frames sharded over {world} GPU(s), no data-path collective",
+                "parallelism": (f"{'streams' if wl['layout'] == 'streams' else 'frames'} sharded over {world} "
+                                f"GPU(s) ({wl['layout']}), no data-path collective"),
                 "compression_ratio": round(comp_bytes / (nf * 2 * n), 4),
             },
             "bitexact_vs_reference": bitexact,

@@ -43,6 +43,12 @@ enum cmp_gpu_sample_type {
 #define CMP_GPU_AUTO_RICE 0x1u /* GOLOMB_ZERO passes other than IWT: choose g = 2^k per frame
 				* (k in [0,15], fewest payload bits, ties to smaller k) instead
 				* of the configured encoder parameter; build-defined extension */
+#define CMP_GPU_HOST_STEPPED 0x2u /* batches that can fall back or fail: step the context state
+				   * machine on the host (one synchronisation per acquisition step)
+				   * instead of on the device; same output, for comparisons */
+#define CMP_GPU_STEPWISE 0x4u     /* MODEL contexts: one launch per acquisition step instead of
+				   * every acquisition in one launch with the models kept on
+				   * the chip; same output, for comparisons */
 
 struct cmp_gpu_batch {
 	enum cmp_gpu_sample_type type;
@@ -54,6 +60,11 @@ struct cmp_gpu_batch {
 	uint32_t dst_capacity;  /* bytes available per frame */
 	uint32_t *sizes;        /* device [num frames]: frame size or error value */
 	uint32_t flags;
+	uint8_t *draws;         /* optional, HOST [num frames]: timestamp-callback draws each frame made
+				 * (0: it carries its context's identifier; 1: a reset; 3 or 2: a
+				 * primary or secondary pass that fell back, cmp.c:342-393), for
+				 * assigning identifiers across processes (shard.py); valid when the
+				 * call returns */
 };
 
 struct cmp_gpu_engine;

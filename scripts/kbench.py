@@ -15,6 +15,10 @@ import bench  # noqa: E402
 pkg = bench.load_pkg()
 api = pkg.cmpapi
 lib = pkg.load()
+if os.environ.get("AIRS_DBG"):  # ablation builds (-DAIRS_ABLATE=1) only: enc_common.h DBG() switches
+    import ctypes
+    lib.lib.airs_dev_set_debug.argtypes = [ctypes.c_uint32, ctypes.c_char_p]
+    lib.lib.airs_dev_set_debug(int(os.environ["AIRS_DBG"]), os.environ.get("AIRS_DBGTS_PATH", "").encode())
 wl = dict(bench.WORKLOADS[sys.argv[1]])
 if os.environ.get("AIRS_KB_FRAMES"):  # scaling probe: more frames of the same shape (no golden digest)
     wl["fpc"] = int(os.environ["AIRS_KB_FRAMES"])

@@ -44,15 +44,22 @@ def _work_size(lib, api, params, nbytes):
     return 0 if api.is_error(w) else w
 
 
+def _per_ctx(params, nctx):
+    """one params for every context, or a list of per-context params"""
+    return list(params) if isinstance(params, (list, tuple)) else [params] * nctx
+
+
 def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000):
     sb = 4 if kind == "i16_in_i32" else 2
+    pcs = _per_ctx(params, nctx)
     lib.set_timestamp_func(_ts_counter(ts_start))
     try:
-        wbs = _work_size(lib, api, params, n * sb)
+        wbs = max(_work_size(lib, api, p, n * sb) for p in pcs)
         ctxs = [api.CmpContext() for _ in range(nctx)]
         wbs_bufs = [api.aligned_empty(max(wbs, 2), fill=0) for _ in range(nctx)]
         for c in range(nctx):
-            r = lib.initialise(ctxs[c], params, wbs_bufs[c] if wbs else None, wbs)
+            w = _work_size(lib, api, pcs[c], n * sb)
+            r = lib.initialise(ctxs[c], pcs[c], wbs_bufs[c] if w else None, w)
             assert not api.is_error(r), api.error_name(r)
         frames = []
         for c in range(nctx):
@@ -67,9 +74,10 @@ def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=500
         lib.set_timestamp_func(None)
 
 
-def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000):
+def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000, flags=0):
     import torch
     sb = 4 if kind == "i16_in_i32" else 2
+    pcs = _per_ctx(params, nctx)
     nf = nctx * fpc
     stride = n * sb
     host_src = np.concatenate([np.ascontiguousarray(s).view(np.uint8) for s in srcs])
@@ -79,16 +87,17 @@ def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start
     sizes = torch.zeros(nf, dtype=torch.int32, device="cuda")
     lib.set_timestamp_func(_ts_counter(ts_start))
     try:
-        wbs = _work_size(lib, api, params, stride)
+        wbs = max(_work_size(lib, api, p, stride) for p in pcs)
         wstride = (max(wbs, 2) + 15) // 16 * 16
         work = torch.zeros(nctx * wstride, dtype=torch.uint8, device="cuda")
         ctxs = (api.CmpContext * nctx)()
         for c in range(nctx):
-            r = lib.initialise(ctxs[c], params, (work.data_ptr() + c * wstride) if wbs else None, wbs)
+            w = _work_size(lib, api, pcs[c], stride)
+            r = lib.initialise(ctxs[c], pcs[c], (work.data_ptr() + c * wstride) if w else None, w)
             assert not api.is_error(r), api.error_name(r)
         torch.cuda.synchronize()
         r = eng.compress(ctxs, fpc, kind, src.data_ptr(), stride, stride, dst.data_ptr(), dstride, cap,
-                         sizes.data_ptr(), 0)
+                         sizes.data_ptr(), flags)
         assert r == 0, api.error_name(r)
         assert eng.synchronize() == 0
         sz = sizes.cpu().numpy().astype(np.uint32)

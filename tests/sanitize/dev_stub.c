@@ -117,6 +117,53 @@ uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L)
 	return 0;
 }
 
+/* the walk needs n % 4096 == 0 and 16-byte aligned inputs; the stub checks
+ * the same so that the host's applicability test is exercised as written */
+int airs_dev_walk_supported(const struct airs_walk *w)
+{
+	if (!w || !w->n || w->n % 4096u || !w->num_ctx || !w->fpc || (w->sample_bytes != 2 && w->sample_bytes != 4))
+		return 0;
+	if (((uintptr_t)w->src & 15u) || (w->src_stride & 15u))
+		return 0;
+	return w->model_ptrs || !(((uintptr_t)w->model & 15u) || (w->model_stride & 15u));
+}
+
+unsigned long stub_walk_calls;
+
+uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_walk *w)
+{
+	if (!e || !airs_dev_walk_supported(w) || !w->status)
+		return ERRV(10u);
+	stub_walk_calls++;
+	for (uint32_t c = 0; c < w->num_ctx; c++) {
+		uint8_t *m = w->model_ptrs ? (uint8_t *)(uintptr_t)w->model_ptrs[c]
+					   : (uint8_t *)w->model + (uint64_t)c * w->model_stride;
+		m[0] ^= 1u; /* touch both ends of the model */
+		m[2u * w->n - 1u] ^= 1u;
+		if (w->seq0s)
+			(void)w->seq0s[c];
+		for (uint32_t a = 0; a < w->fpc; a++) {
+			const uint32_t f = c * w->fpc + a;
+			const uint64_t h = mix(e->salt++ ^ ((uint64_t)f << 32) ^ w->n);
+			const uint8_t *src = (const uint8_t *)w->src + (uint64_t)f * w->src_stride;
+			volatile uint8_t sink = src[0] ^ src[(uint64_t)w->n * w->sample_bytes - 1u];
+			(void)sink;
+			uint32_t size = 16u + (uint32_t)(h % (3ull * w->n + 8u));
+			uint8_t *dst = (uint8_t *)w->dst + (uint64_t)f * w->dst_stride;
+			if (w->ids)
+				(void)w->ids[f];
+			if (w->checksum_enabled && w->checksums)
+				(void)w->checksums[f];
+			if (size > w->cap)
+				size = w->cap;
+			memset(dst, 0, 16);
+			dst[size - 1u] = 0x5A;
+			w->status[f] = size;
+		}
+	}
+	return 0;
+}
+
 uint32_t airs_dev_encode_stream(struct airs_dev_engine *e, const void *src, uint32_t sample_bytes, uint32_t n,
 				uint32_t preprocessing, uint32_t encoder_type, uint32_t encoder_param,
 				uint32_t outlier_param, void *dst, uint32_t cap, uint32_t *status)

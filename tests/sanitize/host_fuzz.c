@@ -18,6 +18,7 @@
 
 static uint64_t g_rng;
 /* outcome counters: the run must reach the interesting paths */
+extern unsigned long stub_walk_calls; /* dev_stub.c */
 static uint32_t n_init_ok, n_frames_ok, n_frames_err, n_batch_ok, n_batch_frames_ok, n_batch_fallback_cap,
 	n_stream_ok;
 
@@ -118,7 +119,9 @@ static void fuzz_batch(struct cmp_gpu_engine *eng)
 	struct cmp_params p;
 	const uint32_t nctx = 1u + pick(4), fpc = 1u + pick(5), nf = nctx * fpc;
 	const uint32_t type = pick(3), sb = type == 2 ? 4u : 2u;
-	const uint32_t n = 1u + pick(pick(2) ? 40 : 3000);
+	/* a quarter of the batches have whole 4096-sample segments: the MODEL
+	 * walk path (airs_dev_walk) becomes applicable */
+	const uint32_t n = pick(4) ? 1u + pick(pick(2) ? 40 : 3000) : 4096u * (1u + pick(2));
 	struct cmp_context *ctx = calloc(nctx, sizeof(*ctx));
 	uint8_t **work = calloc(nctx, sizeof(*work));
 	uint32_t *sizes = calloc(nf, 4u), c, wbs, ok = 1;
@@ -128,6 +131,7 @@ static void fuzz_batch(struct cmp_gpu_engine *eng)
 	uint64_t dstride;
 	uint8_t *dst;
 	struct cmp_gpu_batch b;
+	uint8_t *draws;
 
 	random_params(&p);
 	for (uint64_t i = 0; i < stride * nf; i++)
@@ -154,7 +158,10 @@ static void fuzz_batch(struct cmp_gpu_engine *eng)
 	b.dst_stride = dstride;
 	b.dst_capacity = cap;
 	b.sizes = sizes;
-	b.flags = pick(2) ? CMP_GPU_AUTO_RICE : 0u;
+	b.flags = (pick(2) ? CMP_GPU_AUTO_RICE : 0u) | (pick(4) ? 0u : CMP_GPU_HOST_STEPPED) |
+		  (pick(4) ? 0u : CMP_GPU_STEPWISE);
+	draws = pick(2) ? calloc(nf, 1) : NULL;
+	b.draws = draws;
 	if (ok) {
 		if (!cmp_is_error(cmp_gpu_compress(eng, ctx, nctx, fpc, &b))) {
 			n_batch_ok++;
@@ -193,6 +200,7 @@ static void fuzz_batch(struct cmp_gpu_engine *eng)
 	free(sizes);
 	free(src);
 	free(dst);
+	free(draws);
 }
 
 /* CLI --params grammar: valid strings, mutated and truncated */
@@ -240,8 +248,8 @@ int main(int argc, char **argv)
 	}
 	cmp_gpu_engine_destroy(eng);
 	printf("host_fuzz: %u iterations clean: %u contexts initialised, host frames %u ok / %u errors, "
-	       "%u batches (%u frames ok, %u with fallback enabled), %u streams\n",
+	       "%u batches (%u frames ok, %u with fallback enabled), %u streams, %lu walks\n",
 	       iters, n_init_ok, n_frames_ok, n_frames_err, n_batch_ok, n_batch_frames_ok, n_batch_fallback_cap,
-	       n_stream_ok);
+	       n_stream_ok, stub_walk_calls);
 	return 0;
 }

@@ -23,28 +23,24 @@ def eng(prod):
 
 
 @pytest.fixture(params=["device", "host"])
-def exact_mode(request, monkeypatch):
-    """Batches that can fall back or fail run the context state machine on
-    the GPU (batch_device_exact) unless AIRS_HOST_EXACT=1 selects the
-    host-stepped path (batch_exact); both must equal the call loop."""
-    if request.param == "host":
-        monkeypatch.setenv("AIRS_HOST_EXACT", "1")
-    else:
-        monkeypatch.delenv("AIRS_HOST_EXACT", raising=False)
-    return request.param
+def exact_mode(request):
+    """Batch flags: batches that can fall back or fail run the context state
+    machine on the GPU (batch_device_exact) unless CMP_GPU_HOST_STEPPED selects
+    the host-stepped path (batch_exact); both must equal the call loop."""
+    return api.GPU_HOST_STEPPED if request.param == "host" else 0
 
 
-def _compare(prod, eng, orc, trial):
+def _compare(prod, eng, orc, trial, flags):
     params, kind, n, nctx, fpc, cap, srcs = bs.make_case(api, trial)
     want = bs.run_batch_host(orc, api, params, kind, n, nctx, fpc, cap, srcs)
-    got = bs.run_batch_gpu(prod, eng, api, params, kind, n, nctx, fpc, cap, srcs)
+    got = bs.run_batch_gpu(prod, eng, api, params, kind, n, nctx, fpc, cap, srcs, flags=flags)
     return got == want, want
 
 
 def test_batch_vs_call_loop(prod, eng, orc, exact_mode):
     bad, fallbacks, errors = [], 0, 0
     for trial in range(300):
-        ok, want = _compare(prod, eng, orc, trial)
+        ok, want = _compare(prod, eng, orc, trial, exact_mode)
         frames = want[0]
         errors += sum(api.is_error(r) for r, _ in frames)
         params = bs.make_case(api, trial)[0]
@@ -72,7 +68,7 @@ def test_batch_fallback_identifiers(prod, eng, orc, exact_mode):
         srcs = [rng.integers(0, 65536, n).astype(np.uint16) for _ in range(nctx * fpc)]
         cap = 26 + 6 * n
         want = bs.run_batch_host(orc, api, params, "u16", n, nctx, fpc, cap, srcs)
-        got = bs.run_batch_gpu(prod, eng, api, params, "u16", n, nctx, fpc, cap, srcs)
+        got = bs.run_batch_gpu(prod, eng, api, params, "u16", n, nctx, fpc, cap, srcs, flags=exact_mode)
         assert got == want
         assert all(r == 16 + 2 * n + 4 for r, _ in want[0])
 
@@ -97,7 +93,7 @@ def test_batch_size_field_overflow_vs_call_loop(prod, eng, orc, exact_mode):
     cap = 26 + 6 * n
     want = bs.run_batch_host(orc, api, params, "u16", n, nctx, fpc, cap, srcs)
     assert api.error_name(want[0][0][0]) == "HDR_CMP_SIZE_TOO_LARGE", want[0][0][0]
-    got = bs.run_batch_gpu(prod, eng, api, params, "u16", n, nctx, fpc, cap, srcs)
+    got = bs.run_batch_gpu(prod, eng, api, params, "u16", n, nctx, fpc, cap, srcs, flags=exact_mode)
     assert got == want
 
 
@@ -133,7 +129,36 @@ def test_batch_model_fallback_cfg5_shape(prod, eng, orc, exact_mode, kind):
     want = bs.run_batch_host(orc, api, params, kind, n, nctx, fpc, cap, srcs)
     nfb = sum(1 for r, b in want[0] if b is not None and api.parse_header(b)["encoder_type"] == 0)
     assert nfb > 10, nfb
-    got = bs.run_batch_gpu(prod, eng, api, params, kind, n, nctx, fpc, cap, srcs)
+    got = bs.run_batch_gpu(prod, eng, api, params, kind, n, nctx, fpc, cap, srcs, flags=exact_mode)
+    assert got == want
+
+
+def test_batch_mixed_fallback_model_contexts(prod, eng, orc):
+    """contexts with and without the uncompressed fallback
+    in one batch (different parameters: the host-stepped path), with
+    dst_capacity equal to the raw frame size so that both kinds share that
+    capacity.  A MODEL secondary frame that runs out of room stops updating the
+    model at the failing sample when its context cannot fall back
+    (cmp.c:296-311), and is replaced by a raw frame (whole model) when it
+    can.  Frames, context states and work buffers equal the call loop."""
+    import numpy as np
+    P = api.CmpParams
+    base = dict(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16,
+                secondary_iterations=5, secondary_preprocessing=3, secondary_encoder_type=2,
+                secondary_encoder_param=8, secondary_encoder_outlier=107, model_rate=11)
+    rng = np.random.default_rng(77)
+    n, nctx, fpc = 5000, 4, 6
+    params = [P(**base, uncompressed_fallback_enabled=c % 2) for c in range(nctx)]
+    srcs = []
+    for c in range(nctx):
+        walk = np.cumsum(rng.integers(-3, 4, n))
+        for a in range(fpc):
+            v = rng.integers(-32768, 32768, n) if (c + a) % 3 == 2 else walk + rng.integers(-4, 5, n)
+            srcs.append((v.astype(np.int64) & 0xFFFF).astype(np.uint16))
+    cap = 16 + 2 * n  # the raw frame size: what fallback contexts use as first-attempt capacity
+    want = bs.run_batch_host(orc, api, params, "u16", n, nctx, fpc, cap, srcs)
+    assert sum(api.is_error(r) for r, _ in want[0]) > 2  # fallback-less contexts fail
+    got = bs.run_batch_gpu(prod, eng, api, params, "u16", n, nctx, fpc, cap, srcs)
     assert got == want
 
 

@@ -34,8 +34,9 @@ def test_host_code_clean_under_asan_ubsan(fuzz_bin, seed):
     assert r.returncode == 0, report[-4000:]
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, report[-4000:]
     m = re.search(r"(\d+) contexts initialised, host frames (\d+) ok / (\d+) errors, (\d+) batches "
-                  r"\((\d+) frames ok, (\d+) with fallback", r.stdout)
+                  r"\((\d+) frames ok, (\d+) with fallback.* (\d+) walks", r.stdout)
     assert m, r.stdout
-    init, ok, err, batches, bframes, fb = map(int, m.groups())
-    # the run reached the compress paths, their error paths and the planner
-    assert init > 1000 and ok > 1000 and err > 100 and batches > 1000 and fb > 300, m.group(0)
+    init, ok, err, batches, bframes, fb, walks = map(int, m.groups())
+    # the run reached the compress paths, their error paths, the planner and
+    # the MODEL walk (airs_dev_walk)
+    assert init > 1000 and ok > 1000 and err > 100 and batches > 1000 and fb > 300 and walks > 5, m.group(0)

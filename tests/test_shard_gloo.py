@@ -1,8 +1,9 @@
 """Multi-rank path of SURVEY.md 8(e) on CPU: the frame gather to rank 0
-(all_gather of sizes, packing at 8-byte aligned offsets that reads only the
-compressed bytes, batched point-to-point receives into the root buffer,
-f-order table, identifier patch and its refusal for parameter sets whose
-identifiers depend on the outcomes), world size 2 over gloo."""
+(all_gather of sizes and identifier-draw counts, packing at 8-byte aligned
+offsets that reads only the compressed bytes, batched point-to-point
+receives into the root buffer, f-order table, identifiers from the scan of
+the gathered draw counts, and the refusal to patch without them for
+parameter sets whose draws depend on the outcomes), world size 2 over gloo."""
 import socket
 
 import pytest
@@ -39,3 +40,17 @@ def test_gather_world2_error_value(orc):
 
 def test_gather_world2_patch_refused_with_secondary_passes(orc):
     _spawn(3, 500, "roundrobin", "patch_refused")
+
+
+def test_gather_world2_fallback_identifiers_vs_one_context(orc):
+    """Round-robin frames with the uncompressed fallback (three draws per
+    fallback frame): after the gather every frame, identifier included, equals
+    ONE context's call loop over all frames in global order."""
+    _spawn(8, 700, "roundrobin", "fallback")
+
+
+def test_gather_world2_streams_model_vs_call_loop(orc):
+    """Streams of 5 frames (MODEL secondary passes, fallback enabled) sharded
+    s mod 2: every gathered frame, identifier included, equals one process's
+    c-major call loop over all the streams' contexts."""
+    _spawn(10, 600, "streams", "streams")
