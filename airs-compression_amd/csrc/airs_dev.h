@@ -48,13 +48,13 @@ struct airs_launch {
 	uint32_t encoder_param;  /* Golomb g (ignored for UNCOMPRESSED) */
 	uint32_t outlier_param;  /* user outlier (GOLOMB_MULTI) */
 	const uint32_t *frame_g; /* device, optional per-frame g (all powers of two) */
-	/* CMP_GPU_AUTO_RICE (GOLOMB_ZERO): g = 2^k per frame by the build-defined
-	 * rule.  Frames of a few segments choose k inside the
-	 * encode kernel (one read of the samples); otherwise select_rice_kernel
-	 * writes g into frame_g_scratch (device, one word per batch frame) first */
+	/* CMP_GPU_AUTO_RICE (GOLOMB_ZERO after NONE or DIFF): g = 2^k per frame by
+	 * the build-defined rule.  Frames of a few segments
+	 * choose k inside the encode kernel (one read of the samples); otherwise
+	 * select_rice_kernel writes g for the launch's frames into frame_g_scratch
+	 * (device, one word per batch frame) first */
 	uint32_t auto_rice;
 	uint32_t *frame_g_scratch;
-	uint32_t frame_g_frames;  /* batch frames 0 .. frame_g_frames-1 get a g in the scratch */
 
 	/* model (work buffer): batch frame f's model at model + (f / model_div)*model_stride,
 	 * or model_ptrs[j] (device) */
@@ -180,9 +180,12 @@ uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src, uint64_t 
 			   uint32_t sample_bytes, uint32_t n, uint32_t num_frames,
 			   const uint32_t *frame_list, uint32_t *out);
 
-/* per-frame Rice parameter (build-defined rule): out_g[f] = 2^k */
+/* per-frame Rice parameter (build-defined rule): out_g[f] = 2^k
+ * for the batch frames f = frame_list[j] (AIRS_NO_FRAME: none) or
+ * frame_add + j*frame_mul, j < num_frames */
 uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
 			      uint32_t sample_bytes, uint32_t n, uint32_t num_frames,
+			      const uint32_t *frame_list, uint32_t frame_add, uint32_t frame_mul,
 			      uint32_t preprocessing, uint32_t *out_g);
 
 /* counter-hash synthetic frames (bench/test inputs) */

@@ -402,6 +402,13 @@ static uint64_t frame_worst(uint32_t n)
 	return HDR_MAX_SIZE + CMP_CHECKSUM_SIZE + payload_bound(2u * n) + 8u;
 }
 
+/* an internal failure of the host path (GENERIC), named on stderr */
+static uint32_t host_fail(const char *what)
+{
+	fprintf(stderr, "airscmp: host path: %s failed (%s)\n", what, airs_dev_last_error());
+	return ERRV(GENERIC);
+}
+
 /* Host-pointer frame: stage through device scratch, run, copy back. */
 static uint32_t host_engine(struct cmp_context *ctx, void *dst, uint32_t cap, const struct frame_io *io)
 {
@@ -425,22 +432,22 @@ static uint32_t host_engine(struct cmp_context *ctx, void *dst, uint32_t cap, co
 	d_dst = airs_dev_scratch(dev, SLOT_DST, (size_t)worst);
 	d_status = airs_dev_scratch(dev, SLOT_STATUS, 64);
 	if (!d_src || !d_dst || !d_status)
-		return ERRV(GENERIC);
+		return host_fail("device scratch");
 	if (is_err(airs_dev_h2d(dev, d_src, io->src, (size_t)io->n * io->bytes)))
-		return ERRV(GENERIC);
+		return host_fail("sample upload");
 	if (p.model_mode != AIRS_MODEL_NONE || p.pre == CMP_PREPROCESS_IWT) {
 		/* the work buffer on the device: the model, or the IWT coefficients
 		 * (computed there by the launch, so not uploaded) */
 		d_model = airs_dev_scratch(dev, SLOT_MODEL, (size_t)packed + 16u);
 		if (!d_model)
-			return ERRV(GENERIC);
+			return host_fail("model scratch");
 		if (p.pre != CMP_PREPROCESS_IWT && is_err(airs_dev_h2d(dev, d_model, ctx->work_buf, packed)))
-			return ERRV(GENERIC);
+			return host_fail("model upload");
 	}
 	if (ctx->params.checksum_enabled) {
 		d_ck = airs_dev_scratch(dev, SLOT_CK, 64);
 		if (!d_ck || is_err(airs_dev_checksum(dev, d_src, 0, io->bytes, io->n, 1, NULL, d_ck)))
-			return ERRV(GENERIC);
+			return host_fail("checksum");
 	}
 
 	memset(&L, 0, sizeof(L));
@@ -468,20 +475,22 @@ static uint32_t host_engine(struct cmp_context *ctx, void *dst, uint32_t cap, co
 	L.status = d_status;
 	L.needed = (uint32_t *)d_status + 1;
 	e = airs_dev_encode(dev, &L);
+	if (cmp_get_error_code(e) == CMP_ERR_GENERIC)
+		return host_fail("encode launch");
 	if (is_err(e))
 		return e;
 	if (is_err(airs_dev_d2h(dev, st, d_status, sizeof(st))))
-		return ERRV(GENERIC);
+		return host_fail("status read-back");
 	/* work_buf afterwards holds what the reference leaves there: the model,
 	 * or the IWT coefficients (overwritten by the model where it is stored) */
 	if (d_model && is_err(airs_dev_d2h(dev, ctx->work_buf, d_model, packed)))
-		return ERRV(GENERIC);
+		return host_fail("model read-back");
 	if (is_err(airs_dev_sync(dev)))
-		return ERRV(GENERIC);
+		return host_fail("synchronisation");
 	if (is_err(st[0]))
 		return st[0];
 	if (is_err(airs_dev_d2h(dev, dst, d_dst, st[0])) || is_err(airs_dev_sync(dev)))
-		return ERRV(GENERIC);
+		return host_fail("frame read-back");
 	ctx->sequence_number++;
 	return st[0];
 }
@@ -810,13 +819,13 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 		if (is_err(e))
 			return e;
 	}
-	if ((b->flags & CMP_GPU_AUTO_RICE) && P->enc == CMP_ENCODER_GOLOMB_ZERO && P->pre != CMP_PREPROCESS_IWT) {
+	if ((b->flags & CMP_GPU_AUTO_RICE) && P->enc == CMP_ENCODER_GOLOMB_ZERO &&
+	    (P->pre == CMP_PREPROCESS_NONE || P->pre == CMP_PREPROCESS_DIFF)) {
 		d_g = airs_dev_scratch(dev, SLOT_G, (size_t)nframes_total * 4u);
 		if (!d_g)
 			return ERRV(GENERIC);
 		L.auto_rice = 1;
 		L.frame_g_scratch = d_g;
-		L.frame_g_frames = nframes_total;
 	}
 	L.src = b->src;
 	L.src_stride = b->src_stride;
@@ -1228,10 +1237,10 @@ static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_contex
 			L.encoder_type = Q->enc;
 			L.encoder_param = Q->par;
 			L.outlier_param = Q->outlier_param;
-			if (d_g && Q->enc == CMP_ENCODER_GOLOMB_ZERO) {
+			if (d_g && Q->enc == CMP_ENCODER_GOLOMB_ZERO &&
+			    (Q->pre == CMP_PREPROCESS_NONE || Q->pre == CMP_PREPROCESS_DIFF)) {
 				L.auto_rice = 1;
 				L.frame_g_scratch = d_g;
-				L.frame_g_frames = total;
 			}
 			L.model_mode = mneed ? (which ? AIRS_MODEL_UPDATE : AIRS_MODEL_STORE) : AIRS_MODEL_NONE;
 			L.model_rate = P->model_rate;
@@ -1314,6 +1323,9 @@ static uint32_t batch_walk(struct cmp_gpu_engine *eng, const struct cmp_context 
 
 	if (!model_needed(P) || (P->primary_preprocessing != CMP_PREPROCESS_NONE &&
 				 P->primary_preprocessing != CMP_PREPROCESS_DIFF))
+		return WALK_NO;
+	/* the walk codes with the configured parameters (AUTO_RICE: per-step launches) */
+	if ((b->flags & CMP_GPU_AUTO_RICE) && P->primary_encoder_type == CMP_ENCODER_GOLOMB_ZERO)
 		return WALK_NO;
 	for (c = 0; c < num_ctx; c++)
 		if (!same_params(&ctx[c].params, P))

@@ -32,8 +32,10 @@
 //                d = m - outlier takes idx = 16 + clz(d | 3), whose entry
 //                holds golomb(outlier + lvl) shifted over the 2 (lvl+1) bits
 //                of d (lvl = floor(log2 d) / 2, 0 for d < 4); the codeword is
-//                then m + T as well.  Escapes longer than 32 bits (lvl 7) are
-//                put in two pieces.
+//                then m + T as well.  Escapes longer than 32 bits (any lvl
+//                once golomb(outlier + lvl) itself nears 32 bits, i.e. an
+//                outlier near the upper bound of small g) are put in two
+//                pieces, the escape symbol and d.
 // Other encoders (UNCOMPRESSED, g not a power of two) take code_from_m.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -166,12 +168,14 @@ __device__ __forceinline__ void walk_pack(uint32_t *img, uint32_t excl, const ui
 #pragma unroll
 		for (uint32_t j = 0; j < EPT; j++) {
 			const uint32_t m = half16(mp[j >> 1], j & 1u);
-			const uint2 e = *reinterpret_cast<const uint2 *>(tab + half16(oq[j >> 1], j & 1u));
+			const uint32_t off = half16(oq[j >> 1], j & 1u);
+			const uint2 e = *reinterpret_cast<const uint2 *>(tab + off);
 			if (e.y <= 32u) {
 				pk1.put(m + e.x, e.y);
-			} else { // lvl-7 escape: golomb(outlier + 7), then d in 16 bits
-				pk1.put(e.x, e.y - 16u);
-				pk1.put(m - cd.outlier, 16u);
+			} else { // escape longer than 32 bits: golomb(outlier + lvl), then d in 2 (lvl + 1) bits
+				const uint32_t len2 = 2u * (((31u - ((off >> 3) - 16u)) >> 1) + 1u);
+				pk1.put(e.x, e.y - len2);
+				pk1.put(m - cd.outlier, len2);
 			}
 		}
 	} else {

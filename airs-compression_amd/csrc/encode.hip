@@ -620,12 +620,15 @@ __device__ __forceinline__ uint32_t key_term(uint32_t key, uint32_t k)
 
 template <int W, int PRE>
 __global__ __launch_bounds__(256) void select_rice_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
+							   const uint32_t *flist, uint32_t fadd, uint32_t fmul,
 							   uint32_t *out_g)
 {
 	__shared__ uint32_t hist[4][128];
 	__shared__ uint64_t tot[16];
 	const uint32_t tid = threadIdx.x, wid = tid >> 6;
-	const uint32_t frame = blockIdx.x;
+	const uint32_t frame = flist ? flist[blockIdx.x] : fadd + blockIdx.x * fmul;
+	if (frame == AIRS_NO_FRAME)
+		return;
 	const uint8_t *f = src + (uint64_t)frame * stride;
 	for (uint32_t i = tid; i < 4u * 128u; i += 256u)
 		(&hist[0][0])[i] = 0u;
@@ -1016,8 +1019,11 @@ extern "C" void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t by
 		e->scratch[slot] = nullptr;
 		e->scratch_cap[slot] = 0;
 		size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
-		if (hipMalloc(&e->scratch[slot], want) != hipSuccess)
+		const hipError_t he = hipMalloc(&e->scratch[slot], want);
+		if (he != hipSuccess) {
+			(void)hip_fail(he, "hipMalloc (engine scratch)");
 			return nullptr;
+		}
 		e->scratch_cap[slot] = want;
 	}
 	return e->scratch[slot];
@@ -1271,10 +1277,10 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 				(L->preprocessing == PRE_NONE || L->preprocessing == PRE_DIFF) && spf <= AUTO_MAX_SPF;
 	const uint32_t *frame_g = L->frame_g;
 	if (L->auto_rice && !auto_fused && L->encoder_type == ENC_ZERO) {
-		if (!L->frame_g_scratch)
+		if (!L->frame_g_scratch || (L->preprocessing != PRE_NONE && L->preprocessing != PRE_DIFF))
 			return ERRV(E_GENERIC);
-		r = airs_dev_select_rice(e, L->src, L->src_stride, L->sample_bytes, L->n, L->frame_g_frames,
-					 L->preprocessing, L->frame_g_scratch);
+		r = airs_dev_select_rice(e, L->src, L->src_stride, L->sample_bytes, L->n, L->num_frames, L->frame_list,
+					 L->frame_add, L->frame_mul, L->preprocessing, L->frame_g_scratch);
 		if (r)
 			return r;
 		frame_g = L->frame_g_scratch;
@@ -1531,7 +1537,8 @@ extern "C" uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src
 
 extern "C" uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
 					 uint32_t sample_bytes, uint32_t n, uint32_t num_frames,
-					 uint32_t preprocessing, uint32_t *out_g)
+					 const uint32_t *flist, uint32_t fadd, uint32_t fmul, uint32_t preprocessing,
+					 uint32_t *out_g)
 {
 	if (!e || !n || !num_frames)
 		return ERRV(E_GENERIC);
@@ -1539,17 +1546,17 @@ extern "C" uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *
 	if (sample_bytes == 2) {
 		if (preprocessing == PRE_DIFF)
 			hipLaunchKernelGGL((select_rice_kernel<2, PRE_DIFF>), dim3(num_frames), dim3(256), 0,
-					   e->stream, s, src_stride, n, out_g);
+					   e->stream, s, src_stride, n, flist, fadd, fmul, out_g);
 		else
 			hipLaunchKernelGGL((select_rice_kernel<2, PRE_NONE>), dim3(num_frames), dim3(256), 0,
-					   e->stream, s, src_stride, n, out_g);
+					   e->stream, s, src_stride, n, flist, fadd, fmul, out_g);
 	} else {
 		if (preprocessing == PRE_DIFF)
 			hipLaunchKernelGGL((select_rice_kernel<4, PRE_DIFF>), dim3(num_frames), dim3(256), 0,
-					   e->stream, s, src_stride, n, out_g);
+					   e->stream, s, src_stride, n, flist, fadd, fmul, out_g);
 		else
 			hipLaunchKernelGGL((select_rice_kernel<4, PRE_NONE>), dim3(num_frames), dim3(256), 0,
-					   e->stream, s, src_stride, n, out_g);
+					   e->stream, s, src_stride, n, flist, fadd, fmul, out_g);
 	}
 	HIPCHECK(hipGetLastError());
 	return 0;

@@ -49,7 +49,9 @@ def _per_ctx(params, nctx):
     return list(params) if isinstance(params, (list, tuple)) else [params] * nctx
 
 
-def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000):
+def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000, primary_g=None):
+    """primary_g: optional src -> g, set as the context's primary encoder
+    parameter before each call (the CMP_GPU_AUTO_RICE rule)"""
     sb = 4 if kind == "i16_in_i32" else 2
     pcs = _per_ctx(params, nctx)
     lib.set_timestamp_func(_ts_counter(ts_start))
@@ -65,6 +67,8 @@ def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=500
         for c in range(nctx):
             for a in range(fpc):
                 dst = api.aligned_empty(cap + 64, fill=0xAB)
+                if primary_g is not None:
+                    ctxs[c].params.primary_encoder_param = primary_g(srcs[c * fpc + a])
                 r = lib.compress(kind, ctxs[c], dst, cap, srcs[c * fpc + a])
                 frames.append((r, bytes(dst[:r]) if not api.is_error(r) else None))
         state = [(x.identifier, x.sequence_number, x.model_size, bytes(w[:wbs]))

@@ -295,12 +295,15 @@ uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src, uint64_t 
 }
 
 uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
-			      uint32_t sample_bytes, uint32_t n, uint32_t num_frames, uint32_t preprocessing,
-			      uint32_t *out_g)
+			      uint32_t sample_bytes, uint32_t n, uint32_t num_frames, const uint32_t *frame_list,
+			      uint32_t frame_add, uint32_t frame_mul, uint32_t preprocessing, uint32_t *out_g)
 {
 	(void)e, (void)src, (void)src_stride, (void)sample_bytes, (void)n, (void)preprocessing;
-	for (uint32_t f = 0; f < num_frames; f++)
-		out_g[f] = 32u;
+	for (uint32_t j = 0; j < num_frames; j++) {
+		const uint32_t f = frame_list ? frame_list[j] : frame_add + j * frame_mul;
+		if (f != 0xFFFFFFFFu)
+			out_g[f] = 32u;
+	}
 	return 0;
 }
 

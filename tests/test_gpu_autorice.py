@@ -143,3 +143,38 @@ def test_autorice_k_range(prod, eng, orc, orc_ext):
     assert [_mask(g) for g in got] == [_mask(w) for w in want]
     ks = {api.parse_header(g)["encoder_param"].bit_length() - 1 for g in got}
     assert len(ks) >= 12, sorted(ks)
+
+
+AUTO_BATCH = [  # (kind, n, fallback, flags beyond AUTO_RICE)
+    ("u16", AUTO_MAX_SPF * SEG16 + 100, 1, 0),  # device exact mode, select_rice_kernel per launch
+    ("u16", AUTO_MAX_SPF * SEG16 + 100, 1, 0x2),  # the same, host-stepped
+    ("i16_in_i32", 3 * SEG32 + 5, 1, 0),  # device exact mode, k chosen in the encode kernel
+    ("i16", 2 * SEG16, 0, 0),  # asynchronous mode (one launch per acquisition step: no walk)
+]
+
+
+@pytest.mark.parametrize("kind,n,fallback,extra", AUTO_BATCH)
+def test_autorice_model_batch(prod, eng, orc, orc_ext, kind, n, fallback, extra):
+    """AUTO_RICE in multi-context batches with a MODEL secondary pass: the
+    primary (DIFF) passes take the per-frame g of the rule, the MODEL passes
+    keep their configured g; contexts, models and fallbacks as the call loop
+    with that g set before each call (identifiers included, unmasked).  Each
+    launch selects g for its own frames only (select_rice_kernel over the
+    launch's frame list)."""
+    import batch_scenarios as bs
+    rng = np.random.default_rng(n + extra)
+    nctx, fpc = 2, 5
+    frames = _frames(rng, kind, n, nctx * fpc, extreme=False)
+    prm = P(primary_preprocessing=1, primary_encoder_type=api.ENCODER_GOLOMB_ZERO, primary_encoder_param=4,
+            secondary_iterations=2, secondary_preprocessing=3, secondary_encoder_type=api.ENCODER_GOLOMB_ZERO,
+            secondary_encoder_param=8, model_rate=9, checksum_enabled=1, uncompressed_fallback_enabled=fallback)
+    cap = 26 + 6 * n
+
+    def primary_g(x):
+        return 1 << orc_ext.orc_select_rice_k(np.ascontiguousarray(x).ctypes.data, n,
+                                              1 if kind == "i16_in_i32" else 0, 1, None)
+    want = bs.run_batch_host(orc, api, prm, kind, n, nctx, fpc, cap, frames, primary_g=primary_g)
+    got = bs.run_batch_gpu(prod, eng, api, prm, kind, n, nctx, fpc, cap, frames, flags=1 | extra)
+    assert got[1] == want[1]
+    bad = [f for f in range(nctx * fpc) if got[0][f] != want[0][f]]
+    assert not bad, f"frames {bad} differ"
