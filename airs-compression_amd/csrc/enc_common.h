@@ -321,6 +321,31 @@ __device__ __forceinline__ uint32_t zigzag_pk(uint32_t u)
 	return unpk((x << (u16x2)(1)) ^ __builtin_bit_cast(u16x2, __builtin_bit_cast(i16x2, x) >> (i16x2)(15)));
 }
 
+// MODEL update of a sample pair (reference cmp.c:120-142):
+//   (model*rate + x*(16-rate)) >> 4 = model + ((x - model)*(16-rate) >> 4)
+// exactly (16*model is a multiple of 16; >> is the floor).  x and model are
+// sign-extended (i16) or zero-extended (u16); flip = 0x80008000 for i16 turns
+// the signed difference into one of zero-extended halves (sext(v) =
+// zext(v ^ 0x8000) - 0x8000), 0 for u16.  |x - model| < 2^17 and r1 <= 16, so
+// the product fits a 24-bit multiply; only the low 16 bits are kept.
+// The same on zero-extended halves (u16, or both operands flipped):
+// (x - model) per half, 24-bit multiply, floor shift, add back.
+__device__ __forceinline__ uint32_t model_update_zx(uint32_t x, uint32_t model, int32_t r1)
+{
+	const int32_t d0 = (int32_t)(x & 0xFFFFu) - (int32_t)(model & 0xFFFFu);
+	const int32_t d1 = (int32_t)(x >> 16) - (int32_t)(model >> 16);
+	const int32_t n0 = (int32_t)(model & 0xFFFFu) + (__mul24(d0, r1) >> 4);
+	const int32_t n1 = (int32_t)(model >> 16) + (__mul24(d1, r1) >> 4);
+	return __builtin_amdgcn_perm((uint32_t)n1, (uint32_t)n0, 0x05040100u);
+}
+
+// flip = 0x80008000 for i16, 0 for u16; the result is the model itself
+// (flipping both operands and the result: (m ^ f) + t = (m + t) ^ f mod 2^16)
+__device__ __forceinline__ uint32_t model_update_pk(uint32_t x, uint32_t model, uint32_t flip, int32_t r1)
+{
+	return model_update_zx(x ^ flip, model ^ flip, r1) ^ flip;
+}
+
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // Bit packer into an LDS image.  `nb` is a bit position in the LDS address
@@ -440,9 +465,16 @@ struct WArgs {
 	uint32_t cap, iters, seq0, epoch;
 	uint32_t g_p, outl_p, g_s, outl_s;
 	uint32_t model_rate, is_unsigned, checksum, img_words;
+	uint32_t dbg;    // ablation builds: AIRS_DBG switches (0 in production)
+	uint64_t *dbgts; // AIRS_DBG bit 65536: 8 realtime stamps per (workgroup, acquisition)
 };
 bool walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
 		 bool rice_s, hipStream_t s);
+// one context per workgroup (frames of walk_ctx_samples() samples); img_words
+// = words of ONE of its two 16384-sample images
+bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p,
+		     uint32_t enc_s, bool rice_s, hipStream_t s);
+uint32_t walk_ctx_samples();
 void stream_encode(const KArgs &k, uint32_t sample_bytes, uint32_t pre, uint32_t enc, bool rice, bool full,
 		   uint32_t grid, hipStream_t s);
 

@@ -346,16 +346,9 @@ __device__ __forceinline__ void encode_segment(const KArgs &a, uint32_t seg_in)
 				if (MODEL == 1) {
 					nmp[MODEL ? c : 0][j] = w[j];
 				} else {
-					uint32_t nm2 = 0u;
-#pragma unroll
-					for (uint32_t h = 0; h < 2; h++) {
-						const uint32_t xv = half16(w[j], h), mv = half16(pm[j], h);
-						const int32_t rate = (int32_t)a.model_rate;
-						const int32_t d = a.is_unsigned ? (int32_t)xv : (int32_t)(int16_t)xv;
-						const int32_t mm = a.is_unsigned ? (int32_t)mv : (int32_t)(int16_t)mv;
-						nm2 |= ((uint32_t)((mm * rate + d * (16 - rate)) >> 4) & 0xFFFFu) << (16u * h);
-					}
-					nmp[MODEL ? c : 0][j] = nm2;
+					// cmp.c:132-142
+					nmp[MODEL ? c : 0][j] = model_update_pk(w[j], pm[j], a.is_unsigned ? 0u : 0x80008000u,
+										16 - (int32_t)a.model_rate);
 				}
 			}
 		}

@@ -77,6 +77,26 @@ __device__ __forceinline__ uint2 walk_table_entry(uint32_t idx, const Coder &c)
 }
 
 
+// Debug timeline (ablation builds, AIRS_DBG bit 65536): per (workgroup,
+// acquisition) 8 slots of the 100 MHz realtime clock: 0 samples in registers,
+// 1 after B1, 2 packed, 3 after B2, 4 after B3 (data wave 0); 5 look-back
+// done, 6 predecessor tail seen (control wave); 7 HW_ID << 32 | XCC_ID.
+// scripts/walk_ts.py summarises it.
+__device__ __forceinline__ void wstamp(const WArgs &a, uint32_t acq, uint32_t slot)
+{
+	if (AIRS_ABLATE && (a.dbg & 65536u) && a.dbgts && (threadIdx.x & 63u) == 0u) {
+		uint64_t t;
+		asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+		a.dbgts[8u * ((uint64_t)blockIdx.x * a.fpc + acq) + slot] = t;
+		if (slot == 0u) {
+			uint32_t hw, xcc;
+			asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+			asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+			a.dbgts[8u * ((uint64_t)blockIdx.x * a.fpc + acq) + 7u] = ((uint64_t)hw << 32) | xcc;
+		}
+	}
+}
+
 __device__ __forceinline__ void lds_barrier()
 {
 	// LDS-only barrier: the data waves' prefetch stays in flight across it
@@ -231,6 +251,11 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		L_img[i] = 0u;
 
 	const uint32_t seq0 = a.seq0s ? a.seq0s[c] : a.seq0;
+	// Samples and model are kept "flipped" (i16: the sign bit of every half
+	// inverted, u16: as they are), so that both sample types take the model
+	// update of zero-extended halves (model_update_zx); residuals are
+	// differences and do not change
+	const uint32_t flip = a.is_unsigned ? 0u : 0x80008000u;
 	// the model of this lane's 16 samples, packed pairs
 	uint32_t mdl[EPT / 2];
 #pragma unroll
@@ -241,10 +266,10 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 #pragma unroll
 		for (uint32_t q = 0; q < EPT / 8; q++) {
 			const uint4 v = mp4[q];
-			mdl[4 * q] = v.x;
-			mdl[4 * q + 1] = v.y;
-			mdl[4 * q + 2] = v.z;
-			mdl[4 * q + 3] = v.w;
+			mdl[4 * q] = v.x ^ flip;
+			mdl[4 * q + 1] = v.y ^ flip;
+			mdl[4 * q + 2] = v.z ^ flip;
+			mdl[4 * q + 3] = v.w ^ flip;
 		}
 	}
 	// prefetch of acquisition 0
@@ -282,18 +307,20 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 			if (W == 2) {
 #pragma unroll
 				for (uint32_t q = 0; q < RW; q++) {
-					w[4 * q] = rn[q].x;
-					w[4 * q + 1] = rn[q].y;
-					w[4 * q + 2] = rn[q].z;
-					w[4 * q + 3] = rn[q].w;
+					w[4 * q] = rn[q].x ^ flip;
+					w[4 * q + 1] = rn[q].y ^ flip;
+					w[4 * q + 2] = rn[q].z ^ flip;
+					w[4 * q + 3] = rn[q].w ^ flip;
 				}
 			} else {
 #pragma unroll
 				for (uint32_t q = 0; q < RW; q++) {
-					w[2 * q] = __builtin_amdgcn_perm(rn[q].y, rn[q].x, 0x05040100u);
-					w[2 * q + 1] = __builtin_amdgcn_perm(rn[q].w, rn[q].z, 0x05040100u);
+					w[2 * q] = __builtin_amdgcn_perm(rn[q].y, rn[q].x, 0x05040100u) ^ flip;
+					w[2 * q + 1] = __builtin_amdgcn_perm(rn[q].w, rn[q].z, 0x05040100u) ^ flip;
 				}
 			}
+			if (wid == 0u)
+				wstamp(a, acq, 0u);
 			const uint32_t prevs = pn;
 			if (acq + 1u < a.fpc)
 				issue(acq + 1u); // lands while this acquisition packs
@@ -302,11 +329,11 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 				if (PRE_P == PRE_DIFF) {
 					wprev = __shfl_up(w[EPT / 2 - 1], 1, 64);
 					if (lane == 0u)
-						wprev = prevs << 16;
+						wprev = (prevs << 16) ^ flip;
 				}
 #pragma unroll
 				for (uint32_t q = 0; q < EPT / 2; q++) {
-					uint32_t u = w[q];
+					uint32_t u = w[q] ^ flip; // NONE: the sample itself
 					if (PRE_P == PRE_DIFF)
 						u = unpk(pk(w[q]) - pk(__builtin_amdgcn_alignbit(w[q], q ? w[q - 1] : wprev, 16)));
 					mp[q] = ENC_P == ENC_RAW ? u : zigzag_pk(u);
@@ -314,20 +341,12 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 				}
 				T = walk_lengths<ENC_P, RICE_P>(mp, oq, cp, fast_p, tab_p);
 			} else {
-				const int32_t rate = (int32_t)a.model_rate;
+				const int32_t r1 = 16 - (int32_t)a.model_rate;
 #pragma unroll
 				for (uint32_t q = 0; q < EPT / 2; q++) {
 					const uint32_t u = unpk(pk(w[q]) - pk(mdl[q])); // preprocess.c:406-411
 					mp[q] = ENC_S == ENC_RAW ? u : zigzag_pk(u);
-					uint32_t nm = 0u; // cmp.c:132-142
-#pragma unroll
-					for (uint32_t h = 0; h < 2u; h++) {
-						const uint32_t xv = half16(w[q], h), mv = half16(mdl[q], h);
-						const int32_t d = a.is_unsigned ? (int32_t)xv : (int32_t)(int16_t)xv;
-						const int32_t mm = a.is_unsigned ? (int32_t)mv : (int32_t)(int16_t)mv;
-						nm |= ((uint32_t)((mm * rate + d * (16 - rate)) >> 4) & 0xFFFFu) << (16u * h);
-					}
-					mdl[q] = nm;
+					mdl[q] = model_update_zx(w[q], mdl[q], r1); // cmp.c:132-142
 				}
 				T = walk_lengths<ENC_S, RICE_S>(mp, oq, cs, fast_s, tab_s);
 			}
@@ -342,6 +361,8 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		lds_barrier(); // B1: wave totals
 		const uint32_t w0 = s_wsum[0], w1 = s_wsum[1], w2 = s_wsum[2], w3 = s_wsum[3];
 		const uint32_t A = __builtin_amdgcn_readfirstlane(w0 + w1 + w2 + w3);
+		if (wid == 0u)
+			wstamp(a, acq, 1u);
 		if (data) {
 			excl += (wid > 0u ? w0 : 0u) + (wid > 1u ? w1 : 0u) + (wid > 2u ? w2 : 0u);
 			// ---- pack into the image ----------------------------------------
@@ -400,6 +421,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 				P = sum;
 				if (lane == 0u)
 					gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (P + A));
+				wstamp(a, acq, 5u);
 				// the predecessor's last 32 bits (published after its packing)
 				uint64_t tv = 0ull;
 				if (lane == 0u) {
@@ -414,13 +436,18 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 					}
 				}
 				pred = (uint32_t)__shfl(tv, 0, 64);
+				wstamp(a, acq, 6u);
 			}
 			if (lane == 0u) {
 				s_ctl[0] = P;
 				s_ctl[1] = pred;
 			}
 		}
+		if (wid == 0u)
+			wstamp(a, acq, 2u);
 		lds_barrier(); // B2: packed image, offset and predecessor bits
+		if (wid == 0u)
+			wstamp(a, acq, 3u);
 		const uint32_t P = __builtin_amdgcn_readfirstlane(s_ctl[0]);
 		const uint32_t pred = __builtin_amdgcn_readfirstlane(s_ctl[1]);
 		const uint32_t r = P & 31u, g0 = P >> 5;
@@ -486,6 +513,8 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 						   : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
 		}
 		lds_barrier(); // B3: the image was read
+		if (wid == 0u)
+			wstamp(a, acq, 4u);
 		// clear what this acquisition used (words 0 .. (A+31)/32 - 1, and the
 		// one after for the flush)
 		const uint32_t nw = (A + 63u) >> 5;
@@ -498,7 +527,275 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		uint4 *mo = reinterpret_cast<uint4 *>(mbase + first);
 #pragma unroll
 		for (uint32_t q = 0; q < EPT / 8; q++)
-			mo[q] = make_uint4(mdl[4 * q], mdl[4 * q + 1], mdl[4 * q + 2], mdl[4 * q + 3]);
+			mo[q] = make_uint4(mdl[4 * q] ^ flip, mdl[4 * q + 1] ^ flip, mdl[4 * q + 2] ^ flip, mdl[4 * q + 3] ^ flip);
+	}
+}
+
+// ---------------------------------------------------------------------
+// One context per workgroup (walk_ctx_kernel): 1024 threads walk every
+// acquisition of ONE context, CH chunks of 16384 samples per frame (frames of
+// CH * 16384 samples).  A frame never leaves the workgroup, so the chunks'
+// bit offsets are a running sum inside it: no look-back, no granule, no
+// handoff between workgroups (the segment walk above pays two handoffs per
+// acquisition step, which serialise the 16 segments of a context).
+//   * lane t owns samples [16t, 16t+16) of each chunk and keeps their model
+//     in registers (CH x 8 packed VGPRs);
+//   * the samples of the chunk two steps ahead are loaded while a chunk is
+//     coded (two register sets);
+//   * each chunk is packed into one of two LDS images at its frame bit offset
+//     mod 32, so image word i IS frame word (P >> 5) + i: the store needs no
+//     funnel shift; the chunk's partial last word is carried into the next
+//     chunk's image word 0 (the frame's first chunk starts with header bytes
+//     20-21);
+//   * two barriers per chunk: wave totals (B1), packed image (B2).
+// ---------------------------------------------------------------------
+#define CW_THREADS 1024u
+#define CW_WAVES (CW_THREADS / 64u)
+#define CW_CHUNK (CW_THREADS * EPT)
+// register sets of prefetched samples (1: the next chunk is loaded while one
+// is coded; 2: the one after it as well)
+#ifndef CW_DEPTH
+#define CW_DEPTH 1
+#endif
+
+template <int W, int PRE_P, int ENC_P, bool RICE_P, int ENC_S, bool RICE_S, int CH>
+__global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
+{
+	static_assert(CH % 2 == 0, "two register sets and two images alternate within a frame");
+	constexpr uint32_t RW = EPT * W / 16u; // uint4 per lane
+	extern __shared__ __attribute__((aligned(16))) uint32_t L_img[];
+	__shared__ uint32_t s_wsum[2][CW_WAVES];
+	__shared__ __attribute__((aligned(16))) uint2 s_tab[2][WTAB];
+
+	const uint32_t tid = threadIdx.x, lane = tid & 63u;
+	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const uint32_t c = blockIdx.x;
+	const uint32_t n = a.n; // CH * CW_CHUNK
+	uint16_t *mbase = reinterpret_cast<uint16_t *>(a.model_ptrs ? (uint8_t *)(uintptr_t)a.model_ptrs[c]
+								    : a.model + (uint64_t)c * a.model_stride);
+	// two images of img_words words, each after a 4-word pad (the packer's
+	// first put may OR the word before its image)
+	uint32_t *const img0 = L_img + 4, *const img1 = L_img + 4 + a.img_words;
+
+	const Coder cp = make_coder<ENC_P>(a.g_p, a.outl_p);
+	const Coder cs = make_coder<ENC_S>(a.g_s, a.outl_s);
+	const bool fast_p = RICE_P && (ENC_P == ENC_MULTI || (ENC_P == ENC_ZERO && cp.k <= 11u));
+	const bool fast_s = RICE_S && (ENC_S == ENC_MULTI || (ENC_S == ENC_ZERO && cs.k <= 11u));
+	if (tid < WTAB) {
+		if (fast_p)
+			s_tab[0][tid] = walk_table_entry<ENC_P>(tid, cp);
+		if (fast_s)
+			s_tab[1][tid] = walk_table_entry<ENC_S>(tid, cs);
+	}
+	for (uint32_t i = tid; i < 2u * a.img_words + 4u; i += CW_THREADS)
+		L_img[i] = 0u;
+
+	const uint32_t seq0 = a.seq0s ? a.seq0s[c] : a.seq0;
+	const uint32_t flip = a.is_unsigned ? 0u : 0x80008000u; // see walk_kernel
+	uint32_t mdl[CH][EPT / 2];
+#pragma unroll
+	for (uint32_t cc = 0; cc < CH; cc++)
+#pragma unroll
+		for (uint32_t q = 0; q < EPT / 2; q++)
+			mdl[cc][q] = 0u;
+	if (seq0 != 0u && seq0 <= a.iters) { // the first frame is a secondary pass
+#pragma unroll
+		for (uint32_t cc = 0; cc < CH; cc++) {
+			const uint4 *mp4 = reinterpret_cast<const uint4 *>(mbase + cc * CW_CHUNK + tid * EPT);
+#pragma unroll
+			for (uint32_t q = 0; q < EPT / 8; q++) {
+				const uint4 v = mp4[q];
+				mdl[cc][4 * q] = v.x ^ flip;
+				mdl[cc][4 * q + 1] = v.y ^ flip;
+				mdl[cc][4 * q + 2] = v.z ^ flip;
+				mdl[cc][4 * q + 3] = v.w ^ flip;
+			}
+		}
+	}
+	// samples of step s (= acquisition s / CH, chunk s % CH): register set
+	// s % CW_DEPTH
+	const uint32_t steps = a.fpc * CH;
+	uint4 rs[CW_DEPTH][RW];
+	uint32_t pv[CW_DEPTH];
+#pragma unroll
+	for (uint32_t d = 0; d < CW_DEPTH; d++)
+		pv[d] = 0u;
+	auto issue = [&](uint32_t set, uint32_t step) {
+		const uint32_t acq = step / CH, cc = step % CH;
+		const uint8_t *fs = a.src + (uint64_t)(c * a.fpc + acq) * a.src_stride;
+		const uint32_t first = cc * CW_CHUNK + tid * EPT;
+		const uint4 *p = reinterpret_cast<const uint4 *>(fs + (size_t)first * W);
+#pragma unroll
+		for (uint32_t q = 0; q < RW; q++)
+			rs[set][q] = p[q];
+		if (PRE_P == PRE_DIFF && lane == 0u && first != 0u)
+			pv[set] = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fs)[first - 1u]
+					 : reinterpret_cast<const uint32_t *>(fs)[first - 1u] & 0xFFFFu;
+	};
+#pragma unroll
+	for (uint32_t d = 0; d < CW_DEPTH; d++)
+		if (d < steps)
+			issue(d, d);
+	__syncthreads(); // tables and the zeroed images
+
+	const char *tab_p = reinterpret_cast<const char *>(s_tab[0]);
+	const char *tab_s = reinterpret_cast<const char *>(s_tab[1]);
+	uint32_t sq = seq0;
+	uint32_t used_prev = 0u; // image words the previous step used (cleared after its B1)
+	for (uint32_t acq = 0; acq < a.fpc; acq++) {
+		const uint32_t f = c * a.fpc + acq;
+		const bool prim = sq == 0u || sq > a.iters; // cmp.c:228-248
+		const uint32_t hseq = prim ? 0u : sq;
+		sq = prim ? 1u : sq + 1u;
+		const uint32_t HB = prim ? hdr_bits(PRE_P, ENC_P) : hdr_bits(PRE_MODEL, ENC_S);
+		const uint32_t enc = prim ? (uint32_t)ENC_P : (uint32_t)ENC_S;
+		// frame bit offset of the chunk, and the bits before it in its first word
+		uint32_t P = HB;
+		uint32_t carry = (HB & 31u) && enc != ENC_RAW ? ((prim ? cp.outlier : cs.outlier) & 0xFFFFu) << 16 : 0u;
+		uint8_t *fdst = a.dst + (uint64_t)f * a.dst_stride;
+		const __amdgpu_buffer_rsrc_t dst_rsrc =
+			__builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(a.cap & ~3u), 0x00020000);
+#pragma unroll
+		for (uint32_t cc = 0; cc < CH; cc++) {
+			const uint32_t step = acq * CH + cc;
+			uint32_t *const img = (cc & 1u) ? img1 : img0;
+			uint32_t *const imgo = (cc & 1u) ? img0 : img1;
+			// ---- phase 1 -----------------------------------------------------
+			uint32_t w[EPT / 2];
+			if (W == 2) {
+#pragma unroll
+				for (uint32_t q = 0; q < RW; q++) {
+					w[4 * q] = rs[cc % CW_DEPTH][q].x ^ flip;
+					w[4 * q + 1] = rs[cc % CW_DEPTH][q].y ^ flip;
+					w[4 * q + 2] = rs[cc % CW_DEPTH][q].z ^ flip;
+					w[4 * q + 3] = rs[cc % CW_DEPTH][q].w ^ flip;
+				}
+			} else {
+#pragma unroll
+				for (uint32_t q = 0; q < RW; q++) {
+					w[2 * q] = __builtin_amdgcn_perm(rs[cc % CW_DEPTH][q].y, rs[cc % CW_DEPTH][q].x, 0x05040100u) ^ flip;
+					w[2 * q + 1] =
+						__builtin_amdgcn_perm(rs[cc % CW_DEPTH][q].w, rs[cc % CW_DEPTH][q].z, 0x05040100u) ^ flip;
+				}
+			}
+			const uint32_t prevs = pv[cc % CW_DEPTH];
+			if (step + CW_DEPTH < steps)
+				issue(cc % CW_DEPTH, step + CW_DEPTH); // lands while the chunks before it are coded
+			uint32_t mp[EPT / 2], oq[EPT / 2];
+			uint32_t T;
+			if (prim) {
+				uint32_t wprev = 0u;
+				if (PRE_P == PRE_DIFF) {
+					wprev = __shfl_up(w[EPT / 2 - 1], 1, 64);
+					if (lane == 0u)
+						wprev = (prevs << 16) ^ flip;
+				}
+#pragma unroll
+				for (uint32_t q = 0; q < EPT / 2; q++) {
+					uint32_t u = w[q] ^ flip;
+					if (PRE_P == PRE_DIFF)
+						u = unpk(pk(w[q]) - pk(__builtin_amdgcn_alignbit(w[q], q ? w[q - 1] : wprev, 16)));
+					mp[q] = ENC_P == ENC_RAW ? u : zigzag_pk(u);
+					mdl[cc][q] = w[q]; // cmp.c:305-306
+				}
+				T = walk_lengths<ENC_P, RICE_P>(mp, oq, cp, fast_p, tab_p);
+			} else {
+				const int32_t r1 = 16 - (int32_t)a.model_rate;
+#pragma unroll
+				for (uint32_t q = 0; q < EPT / 2; q++) {
+					const uint32_t u = unpk(pk(w[q]) - pk(mdl[cc][q])); // preprocess.c:406-411
+					mp[q] = ENC_S == ENC_RAW ? u : zigzag_pk(u);
+					mdl[cc][q] = model_update_zx(w[q], mdl[cc][q], r1); // cmp.c:132-142
+				}
+				T = walk_lengths<ENC_S, RICE_S>(mp, oq, cs, fast_s, tab_s);
+			}
+#pragma unroll
+			for (uint32_t q = 0; q < EPT / 2; q++)
+				asm volatile("" : "+v"(mp[q]), "+v"(oq[q]));
+			const uint32_t inc = wave_incl_scan(T);
+			if (lane == 63u)
+				s_wsum[cc & 1u][wid] = inc;
+			lds_barrier(); // B1: wave totals
+			// the previous chunk's image: stored, its carry taken; clear it
+			for (uint32_t i = tid; i < used_prev; i += CW_THREADS)
+				imgo[i] = 0u;
+			const uint32_t ws = lane < CW_WAVES ? s_wsum[cc & 1u][lane] : 0u;
+			const uint32_t wsc = wave_incl_scan(ws);
+			const uint32_t A = (uint32_t)__builtin_amdgcn_readlane((int)wsc, CW_WAVES - 1);
+			const uint32_t wex = wid ? (uint32_t)__builtin_amdgcn_readlane((int)wsc, (int)wid - 1) : 0u;
+			const uint32_t r = P & 31u;
+			// ---- pack at the chunk's frame bit offset mod 32 ---------------------
+			if (prim)
+				walk_pack<ENC_P, RICE_P>(img, r + wex + inc - T, mp, oq, cp, fast_p, tab_p);
+			else
+				walk_pack<ENC_S, RICE_S>(img, r + wex + inc - T, mp, oq, cs, fast_s, tab_s);
+			if (tid == 0u && r)
+				__hip_atomic_fetch_or(reinterpret_cast<lds_u32 *>((uintptr_t)img), carry, __ATOMIC_RELAXED,
+						      __HIP_MEMORY_SCOPE_WORKGROUP);
+			lds_barrier(); // B2: the packed image
+			// ---- store the whole words, big-endian (frame word (P >> 5) + i) -----
+			const uint32_t end = r + A, nfull = end >> 5;
+			const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)img);
+			const uint32_t g0 = P >> 5;
+			for (uint32_t p = tid; p < (nfull >> 2); p += CW_THREADS) {
+				const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + 4u * p);
+				u32x4 o;
+				o.x = bswap32(wv.x);
+				o.y = bswap32(wv.y);
+				o.z = bswap32(wv.z);
+				o.w = bswap32(wv.w);
+				__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, (int)(4u * (g0 + 4u * p)), 0, 0);
+			}
+			const uint32_t rr = (tid - (nfull >> 2)) & (CW_THREADS - 1u);
+			if (rr < (nfull & 3u)) {
+				const uint32_t jw = (nfull & ~3u) + rr;
+				__builtin_amdgcn_raw_buffer_store_b32(bswap32(Ll[jw]), dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
+			}
+			carry = (end & 31u) ? __builtin_amdgcn_readfirstlane(Ll[nfull]) : 0u;
+			used_prev = nfull + 1u;
+			P += A;
+		}
+		// ---- frame epilogue (cmp.c:314-334) -----------------------------------
+		if (tid == 0u) {
+			const uint32_t endbit = P;
+			if (endbit & 31u) { // zero-padded final bytes (bitstream_flush)
+				const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
+				for (uint32_t b = 0; b < nbytes; b++)
+					if (4u * (endbit >> 5) + b < a.cap)
+						fdst[4u * (endbit >> 5) + b] = (uint8_t)(carry >> (24u - 8u * b));
+			}
+			const uint32_t payload_bytes = (endbit + 7u) >> 3;
+			const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
+			if (a.checksum) {
+				const uint32_t ck = a.checksums[f];
+				for (uint32_t b = 0; b < 4u; b++)
+					if (payload_bytes + b < a.cap)
+						fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
+			}
+			const uint64_t id = a.ids ? a.ids[f] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)acq * a.id_astep;
+			uint32_t h[5];
+			if (prim)
+				header_words(h, size, 2u * n, id, hseq, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
+					     ENC_P == ENC_RAW ? 0u : cp.g, ENC_P == ENC_RAW ? 0u : cp.outlier);
+			else
+				header_words(h, size, 2u * n, id, hseq, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S, a.model_rate,
+					     ENC_S == ENC_RAW ? 0u : cs.g, ENC_S == ENC_RAW ? 0u : cs.outlier);
+			const uint32_t hwords = HB == 176u ? 5u : 4u;
+			for (uint32_t wq = 0; wq < hwords; wq++)
+				if (4u * wq + 4u <= a.cap)
+					*reinterpret_cast<uint32_t *>(fdst + 4u * wq) = bswap32(h[wq]);
+			a.status[f] = size > a.cap ? ERRV(E_DST_TOO_SMALL)
+						   : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
+		}
+	}
+	// the model after the last acquisition, to the work buffer (cmp.c:304-311)
+#pragma unroll
+	for (uint32_t cc = 0; cc < CH; cc++) {
+		uint4 *mo = reinterpret_cast<uint4 *>(mbase + cc * CW_CHUNK + tid * EPT);
+#pragma unroll
+		for (uint32_t q = 0; q < EPT / 8; q++)
+			mo[q] = make_uint4(mdl[cc][4 * q] ^ flip, mdl[cc][4 * q + 1] ^ flip, mdl[cc][4 * q + 2] ^ flip,
+					   mdl[cc][4 * q + 3] ^ flip);
 	}
 }
 
@@ -527,6 +824,48 @@ static bool walk_launch_p(const WArgs &k, uint32_t enc_p, bool rice_p, uint32_t 
 	if (enc_p == ENC_MULTI && rice_p)
 		return walk_launch_s<W, PRE_P, ENC_MULTI, true>(k, enc_s, rice_s, lds, s);
 	return false;
+}
+
+template <int W, int PRE_P, int ENC_P, bool RICE_P>
+static bool walk_ctx_launch_s(const WArgs &k, uint32_t enc_s, bool rice_s, size_t lds, hipStream_t s)
+{
+	const dim3 grid(k.num_ctx), blk(CW_THREADS);
+	if (enc_s == ENC_ZERO && rice_s)
+		hipLaunchKernelGGL((walk_ctx_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 4>), grid, blk, lds, s, k);
+	else if (enc_s == ENC_MULTI && rice_s)
+		hipLaunchKernelGGL((walk_ctx_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 4>), grid, blk, lds, s, k);
+	else
+		return false;
+	return true;
+}
+
+template <int W, int PRE_P>
+static bool walk_ctx_launch_p(const WArgs &k, uint32_t enc_p, bool rice_p, uint32_t enc_s, bool rice_s, size_t lds,
+			      hipStream_t s)
+{
+	if (enc_p == ENC_ZERO && rice_p)
+		return walk_ctx_launch_s<W, PRE_P, ENC_ZERO, true>(k, enc_s, rice_s, lds, s);
+	if (enc_p == ENC_MULTI && rice_p)
+		return walk_ctx_launch_s<W, PRE_P, ENC_MULTI, true>(k, enc_s, rice_s, lds, s);
+	return false;
+}
+
+uint32_t walk_ctx_samples()
+{
+	return 4u * CW_CHUNK;
+}
+
+bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p,
+		     uint32_t enc_s, bool rice_s, hipStream_t s)
+{
+	if (k.n != 4u * CW_CHUNK)
+		return false;
+	const size_t lds = (size_t)(2u * k.img_words + 4u) * 4u;
+	if (sample_bytes == 2)
+		return pre_p == PRE_DIFF ? walk_ctx_launch_p<2, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
+					 : walk_ctx_launch_p<2, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);
+	return pre_p == PRE_DIFF ? walk_ctx_launch_p<4, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
+				 : walk_ctx_launch_p<4, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);
 }
 
 bool walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,

@@ -1054,6 +1054,26 @@ static uint32_t image_words(uint32_t encoder_type, uint32_t g)
 	return (words + 3u) & ~3u;
 }
 
+// Longest codeword (bits) a Rice pass emits with these parameters (the
+// outlier clamped as make_coder does); sizes the context walk's images
+static uint32_t code_max_bits(uint32_t enc, uint32_t g, uint32_t outlier_param)
+{
+	if (enc == ENC_RAW || !g)
+		return enc == ENC_RAW ? 16u : 48u;
+	uint32_t k = 0u;
+	while ((2u << k) <= g && k < 31u)
+		k++;
+	if (enc == ENC_ZERO)
+		return k + 17u;
+	uint64_t limit = (uint64_t)g + (uint64_t)(31u - k) * g;
+	limit = limit > 8u ? limit - 8u : 0u;
+	const uint64_t outl = outlier_param < limit ? outlier_param : limit;
+	const uint64_t nonesc = outl ? ((outl - 1u) >> k) + k + 1u : 0u;
+	const uint64_t esc = outl <= 65535u ? ((outl + 7u) >> k) + k + 1u + 16u : 0u;
+	const uint64_t mb = nonesc > esc ? nonesc : esc;
+	return mb < 48u ? (uint32_t)mb : 48u;
+}
+
 // launch epoch tag of the look-back granules (never 0: zeroed granules never match)
 static uint32_t next_epoch(airs_dev_engine *e)
 {
@@ -1407,6 +1427,12 @@ extern "C" int airs_dev_walk_supported(const struct airs_walk *w)
 	return segs <= 0x7FFFFFFFull && segs * w->fpc <= 0x7FFFFFFFull;
 }
 
+// contexts from which a batch of walk_ctx_samples()-sample frames takes the
+// context walk (one workgroup per context) instead of the segment walk
+#ifndef AIRS_WALK_CTX_MIN
+#define AIRS_WALK_CTX_MIN 128u
+#endif
+
 extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_walk *w)
 {
 	if (!e || !airs_dev_walk_supported(w))
@@ -1453,6 +1479,36 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 	const uint32_t iw_p = image_words(w->enc_p, w->g_p), iw_s = image_words(w->enc_s, w->g_s);
 	k.img_words = (iw_p > iw_s ? iw_p : iw_s) + 4u;
 	k.epoch = next_epoch(e);
+	// one context per workgroup when the frames have its size, there are
+	// enough contexts to fill the CUs, and two images fit the LDS
+	{
+		const uint32_t mbp = code_max_bits(w->enc_p, w->g_p, w->outl_p);
+		const uint32_t mbs = code_max_bits(w->enc_s, w->g_s, w->outl_s);
+		const uint32_t mb = mbp > mbs ? mbp : mbs;
+		const uint32_t cw = ((walk_ctx_samples() / 4u * mb / 32u + 8u) + 3u) & ~3u;
+		if (w->n == walk_ctx_samples() && w->num_ctx >= AIRS_WALK_CTX_MIN && (2u * cw + 4u) * 4u <= 150u * 1024u) {
+			WArgs kc = k;
+			kc.img_words = cw;
+			if (!walk_ctx_encode(kc, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream))
+				return ERRV(E_PARAMS_INVALID);
+			HIPCHECK(hipGetLastError());
+			return 0;
+		}
+	}
+#if AIRS_ABLATE
+	k.dbg = g_dbg;
+	if (g_dbg & 65536) {
+		const size_t need = 8u * (size_t)total * spf;
+		if (e->dbgts_n < need) {
+			(void)hipFree(e->dbgts);
+			e->dbgts_n = need;
+			if (hipMalloc(&e->dbgts, e->dbgts_n * 8u) != hipSuccess)
+				return ERRV(E_GENERIC);
+		}
+		HIPCHECK(hipMemsetAsync(e->dbgts, 0, need * 8u, e->stream));
+		k.dbgts = e->dbgts;
+	}
+#endif
 	if (!walk_encode(k, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream))
 		return ERRV(E_PARAMS_INVALID);
 	HIPCHECK(hipGetLastError());
@@ -1513,7 +1569,9 @@ extern "C" uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src
 	const uint32_t stripes = 2u * n >= 16u ? n / 8u : 0u;
 	const uint32_t S4 = (stripes + 3u) & ~3u;
 	// whole groups of 16 frames x 4 chains
-	uint32_t *Y = (uint32_t *)airs_dev_scratch(e, AIRS_NSLOT - 4, (size_t)grid.x * 64u * S4 * 4u);
+	// (at least one granule: frames under 8 samples have no stripes, and an
+	// empty request would return a slot that was never allocated)
+	uint32_t *Y = (uint32_t *)airs_dev_scratch(e, AIRS_NSLOT - 4, (size_t)grid.x * 64u * S4 * 4u + 16u);
 	if (!Y)
 		return ERRV(E_GENERIC);
 	if (stripes) {

@@ -223,3 +223,35 @@ def test_walk_cfg5_shape(prod, eng, orc, orc_ext):
     want = run_host(orc, [p] * nctx, "i16_in_i32", n, nctx, [(fpc, srcs)], cap)
     got = run_gpu(prod, eng, [p] * nctx, "i16_in_i32", n, nctx, [(fpc, srcs)], cap)
     assert got == want
+
+
+CTX_CASES = [  # (kind, pre_p, enc_p, g_p, o_p, enc_s, g_s, o_s, iters, rate, checksum)
+    ("i16_in_i32", 1, 1, 16, 0, 2, 8, 107, 15, 11, 0),  # BASELINE config 5's parameters
+    ("u16", 0, 2, 64, 42, 1, 4, 0, 1, 16, 1),
+    ("i16", 1, 2, 2, 107, 2, 1024, 60000, 2, 0, 0),  # 48-bit codes: two images do not fit, segment walk
+    ("i16_in_i32", 0, 1, 1, 0, 1, 32768, 0, 7, 5, 1),
+    ("i16", 1, 2, 16, 100, 2, 4, 30, 3, 9, 1),
+]
+
+
+@pytest.mark.parametrize("case", range(len(CTX_CASES)))
+def test_walk_ctx_vs_call_loop(prod, eng, orc, case):
+    """Batches of >= 128 contexts of 64 Ki-sample frames take the context walk
+    (one workgroup per context, walk_ctx_kernel): frames, sizes, context
+    states and work buffers equal the call loop; two calls in a row, so the
+    second starts mid-sequence with the model read back from the work
+    buffers."""
+    kind, pre, ep, gp, op, es, gs, osx, iters, rate, ck = CTX_CASES[case]
+    rng = np.random.default_rng(500 + case)
+    n, nctx = 65536, 128
+    p = P(primary_preprocessing=pre, primary_encoder_type=ep, primary_encoder_param=gp, primary_encoder_outlier=op,
+          secondary_iterations=iters, secondary_preprocessing=3, secondary_encoder_type=es,
+          secondary_encoder_param=gs, secondary_encoder_outlier=osx, model_rate=rate, checksum_enabled=ck)
+    calls = [(2, make_frames(kind, n, nctx * 2, rng)), (1, make_frames(kind, n, nctx, rng))]
+    cap = 26 + 6 * n
+    want = run_host(orc, [p] * nctx, kind, n, nctx, calls, cap)
+    got = run_gpu(prod, eng, [p] * nctx, kind, n, nctx, calls, cap)
+    for ci, ((fw, sw), (fg, sg)) in enumerate(zip(want, got)):
+        bad = [f for f in range(len(fw)) if fw[f] != fg[f]]
+        assert not bad, f"call {ci}: frames {bad[:8]} differ"
+        assert sw == sg, f"call {ci}: context states differ"
