@@ -71,7 +71,7 @@ __device__ __forceinline__ uint32_t auto_term(uint32_t bin, uint32_t k)
 }
 
 template <int W, int PRE, int ENC, bool RICE, int MODEL, bool FULL, bool AUTO = false, bool STREAM = false>
-__device__ __forceinline__ void encode_segment(const KArgs &a, uint32_t seg_in)
+__global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 {
 	// AUTO: the frame's k is chosen here from the samples already in registers
 	// (one read); the frame's segments meet once at the 16-candidate granules,
@@ -114,7 +114,7 @@ __device__ __forceinline__ void encode_segment(const KArgs &a, uint32_t seg_in)
 	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform
 
 	// ---- segment id: dispatch order (or an atomic ticket, debug switch) ----
-	uint32_t seg = seg_in;
+	uint32_t seg = blockIdx.x;
 	if (DBG(4u)) {
 		if (tid == 0)
 			s_misc[0] = atomicAdd(a.ticket, 1u) - a.ticket_base;
@@ -1131,43 +1131,14 @@ __device__ __forceinline__ void encode_segment(const KArgs &a, uint32_t seg_in)
 	}
 }
 
-// Persistent form (experiment, AIRS_PERSIST=1): a grid of co-resident
-// workgroups, workgroup w encoding segments w, w + G, w + 2G, ... so that the
-// stores of one segment drain while the next one loads; a segment still only
-// waits for segments of its frame with a smaller dispatch index, all of
-// which belong to resident workgroups.
-#ifndef AIRS_PERSIST
-#define AIRS_PERSIST 0
-#endif
-template <int W, int PRE, int ENC, bool RICE, int MODEL, bool FULL, bool AUTO = false, bool STREAM = false>
-__global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
-{
-	if (AIRS_PERSIST && a.grid_blocks > gridDim.x) {
-		for (uint32_t s = blockIdx.x; s < a.grid_blocks; s += gridDim.x) {
-			encode_segment<W, PRE, ENC, RICE, MODEL, FULL, AUTO, STREAM>(a, s);
-			__syncthreads(); // the next segment reuses the LDS images
-		}
-	} else {
-		encode_segment<W, PRE, ENC, RICE, MODEL, FULL, AUTO, STREAM>(a, blockIdx.x);
-	}
-}
-
-// Launch an encode kernel over `grid` blocks (segments); AIRS_PERSIST builds
-// launch at most the co-resident workgroups, each walking the blocks.
+// Launch an encode kernel over `grid` blocks (segments).  (A persistent form,
+// co-resident workgroups walking the segments, was measured slower: DESIGN.md
+// 5.2; passing the kernel arguments on to a device function by reference also
+// cost 20 %: the compiler kept them in spilled SGPRs, read back by v_readlane.)
 template <typename Kern>
-static inline void launch_segments(Kern kern, KArgs k, uint32_t grid, size_t lds, hipStream_t s, bool persist)
+static inline void launch_segments(Kern kern, const KArgs &k, uint32_t grid, size_t lds, hipStream_t s)
 {
-	k.grid_blocks = grid;
-	uint32_t g = grid;
-	if (AIRS_PERSIST && persist) {
-		int nb = 0, dev = 0, ncu = 0;
-		if (hipGetDevice(&dev) == hipSuccess &&
-		    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-		    hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, EWG, lds) == hipSuccess && nb > 0 &&
-		    (uint64_t)nb * ncu < grid)
-			g = (uint32_t)nb * (uint32_t)ncu;
-	}
-	hipLaunchKernelGGL(kern, dim3(g), dim3(EWG), lds, s, k);
+	hipLaunchKernelGGL(kern, dim3(grid), dim3(EWG), lds, s, k);
 }
 
 } // namespace airs

@@ -20,9 +20,9 @@ static void stream_go(const KArgs &k, bool full, uint32_t grid, hipStream_t s)
 {
 	const size_t lds = (size_t)seg_images(W, 0) * (k.img_words + 4u) * 4u;
 	if (full)
-		launch_segments(encode_kernel<W, PRE, ENC, RICE, 0, true, false, true>, k, grid, lds, s, true);
+		launch_segments(encode_kernel<W, PRE, ENC, RICE, 0, true, false, true>, k, grid, lds, s);
 	else
-		launch_segments(encode_kernel<W, PRE, ENC, RICE, 0, false, false, true>, k, grid, lds, s, true);
+		launch_segments(encode_kernel<W, PRE, ENC, RICE, 0, false, false, true>, k, grid, lds, s);
 }
 
 template <int W, int PRE>

@@ -103,6 +103,34 @@ __device__ __forceinline__ void lds_barrier()
 	asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Buffer descriptor words of [base, base + bytes): raw buffer, the hardware
+// range check drops stores past `bytes`
+__device__ __forceinline__ u32x4 rsrc_words(const void *base, uint32_t bytes)
+{
+	const uint64_t b = (uint64_t)(uintptr_t)base;
+	u32x4 r;
+	r.x = __builtin_amdgcn_readfirstlane((uint32_t)b);
+	r.y = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32) & 0xFFFFu);
+	r.z = __builtin_amdgcn_readfirstlane(bytes);
+	r.w = 0x00020000u;
+	return r;
+}
+
+// Output stores the compiler does not count.  The walks issue their sample
+// prefetch after the stores of a step; the compiler's wait for the prefetched
+// registers then counts only the loads issued after them, instead of falling
+// back to vmcnt(0) behind a data-dependent number of stores (which would wait
+// for every store and for the prefetch of the step after).
+__device__ __forceinline__ void store_b128_nc(u32x4 v, uint32_t byte_off, u32x4 rsrc)
+{
+	asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen" ::"v"(v), "v"(byte_off), "s"(rsrc) : "memory");
+}
+
+__device__ __forceinline__ void store_b32_nc(uint32_t v, uint32_t byte_off, u32x4 rsrc)
+{
+	asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(v), "v"(byte_off), "s"(rsrc) : "memory");
+}
+
 // one pass's residual-independent coding: table offsets (8 idx per sample,
 // 16-bit halves of oq[]), lengths total of the lane; returns the lane's bits
 template <int ENC, bool RICE>
@@ -558,17 +586,139 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 #define CW_DEPTH 1
 #endif
 
+// the 16 samples of this lane from a register set, as packed flipped pairs
+template <int W>
+__device__ __forceinline__ void cw_pairs(const uint4 (&r)[EPT * W / 16u], uint32_t flip, uint32_t (&w)[EPT / 2])
+{
+	if (W == 2) {
+#pragma unroll
+		for (uint32_t q = 0; q < EPT / 8; q++) {
+			w[4 * q] = r[q].x ^ flip;
+			w[4 * q + 1] = r[q].y ^ flip;
+			w[4 * q + 2] = r[q].z ^ flip;
+			w[4 * q + 3] = r[q].w ^ flip;
+		}
+	} else {
+#pragma unroll
+		for (uint32_t q = 0; q < EPT / 4; q++) {
+			w[2 * q] = __builtin_amdgcn_perm(r[q].y, r[q].x, 0x05040100u) ^ flip;
+			w[2 * q + 1] = __builtin_amdgcn_perm(r[q].w, r[q].z, 0x05040100u) ^ flip;
+		}
+	}
+}
+
+// NONE/DIFF residuals of a flipped pair sequence (ZigZag unless UNCOMPRESSED)
+template <int PRE, int ENC>
+__device__ __forceinline__ void cw_primary(const uint32_t (&w)[EPT / 2], uint32_t prevs, uint32_t flip, uint32_t lane,
+					   uint32_t (&mp)[EPT / 2])
+{
+	uint32_t wprev = 0u;
+	if (PRE == PRE_DIFF) {
+		wprev = __shfl_up(w[EPT / 2 - 1], 1, 64);
+		if (lane == 0u)
+			wprev = (prevs << 16) ^ flip;
+	}
+#pragma unroll
+	for (uint32_t q = 0; q < EPT / 2; q++) {
+		uint32_t u = w[q] ^ flip;
+		if (PRE == PRE_DIFF)
+			u = unpk(pk(w[q]) - pk(__builtin_amdgcn_alignbit(w[q], q ? w[q - 1] : wprev, 16)));
+		mp[q] = ENC == ENC_RAW ? u : zigzag_pk(u);
+	}
+}
+
+// Chunk state of a workgroup walk: the chunk's frame bit offset P, the bits
+// before it in its first word (carry), image words the previous chunk used
+struct CwState {
+	uint32_t P, carry, used_prev;
+};
+
+// One chunk after its lengths: block scan (B1), packing at the frame bit
+// offset mod 32 into img (the carry ORed into word 0), B2, store of the whole
+// words (frame word (P >> 5) + i, big-endian), carry of the partial last
+// word; the previous chunk's image imgo is cleared after B1.
+template <int ENC, bool RICE, uint32_t NT = CW_THREADS>
+__device__ __forceinline__ void cw_chunk(CwState &st, uint32_t *img, uint32_t *imgo, uint32_t (*s_wsum)[NT / 64u],
+					 uint32_t par, uint32_t T, const uint32_t (&mp)[EPT / 2],
+					 const uint32_t (&oq)[EPT / 2], const Coder &cd, bool fast, const char *tab,
+					 u32x4 dst_rsrc)
+{
+	const uint32_t tid = threadIdx.x, lane = tid & 63u;
+	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const uint32_t inc = wave_incl_scan(T);
+	if (lane == 63u)
+		s_wsum[par][wid] = inc;
+	lds_barrier(); // B1: wave totals
+	for (uint32_t i = tid; i < st.used_prev; i += NT)
+		imgo[i] = 0u;
+	const uint32_t ws = lane < (NT / 64u) ? s_wsum[par][lane] : 0u;
+	const uint32_t wsc = wave_incl_scan(ws);
+	const uint32_t A = (uint32_t)__builtin_amdgcn_readlane((int)wsc, (NT / 64u) - 1);
+	const uint32_t wex = wid ? (uint32_t)__builtin_amdgcn_readlane((int)wsc, (int)wid - 1) : 0u;
+	const uint32_t r = st.P & 31u;
+	walk_pack<ENC, RICE>(img, r + wex + inc - T, mp, oq, cd, fast, tab);
+	if (tid == 0u && r)
+		__hip_atomic_fetch_or(reinterpret_cast<lds_u32 *>((uintptr_t)img), st.carry, __ATOMIC_RELAXED,
+				      __HIP_MEMORY_SCOPE_WORKGROUP);
+	lds_barrier(); // B2: the packed image
+	const uint32_t end = r + A, nfull = end >> 5;
+	const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)img);
+	const uint32_t g0 = st.P >> 5;
+	for (uint32_t p = tid; p < (nfull >> 2); p += NT) {
+		const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + 4u * p);
+		u32x4 o;
+		o.x = bswap32(wv.x);
+		o.y = bswap32(wv.y);
+		o.z = bswap32(wv.z);
+		o.w = bswap32(wv.w);
+		store_b128_nc(o, 4u * (g0 + 4u * p), dst_rsrc);
+	}
+	const uint32_t rr = (tid - (nfull >> 2)) & (NT - 1u);
+	if (rr < (nfull & 3u)) {
+		const uint32_t jw = (nfull & ~3u) + rr;
+		store_b32_nc(bswap32(Ll[jw]), 4u * (g0 + jw), dst_rsrc);
+	}
+	st.carry = (end & 31u) ? __builtin_amdgcn_readfirstlane(Ll[nfull]) : 0u;
+	st.used_prev = nfull + 1u;
+	st.P += A;
+}
+
+// Frame epilogue (cmp.c:314-334), one thread: zero-padded final bytes
+// (bitstream_flush), checksum, header dwords, status (and needed)
+__device__ __forceinline__ void cw_epilogue(uint8_t *fdst, uint32_t cap, uint32_t endbit, uint32_t carry, uint32_t HB,
+					    bool checksum, uint32_t ck, const uint32_t (&h4)[5], uint32_t *status,
+					    uint32_t *needed, uint32_t frame, uint32_t size)
+{
+	if (endbit & 31u) {
+		const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
+		for (uint32_t b = 0; b < nbytes; b++)
+			if (4u * (endbit >> 5) + b < cap)
+				fdst[4u * (endbit >> 5) + b] = (uint8_t)(carry >> (24u - 8u * b));
+	}
+	const uint32_t payload_bytes = (endbit + 7u) >> 3;
+	if (checksum)
+		for (uint32_t b = 0; b < 4u; b++)
+			if (payload_bytes + b < cap)
+				fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
+	const uint32_t hwords = HB == 176u ? 5u : 4u;
+	for (uint32_t wq = 0; wq < hwords; wq++)
+		if (4u * wq + 4u <= cap)
+			*reinterpret_cast<uint32_t *>(fdst + 4u * wq) = bswap32(h4[wq]);
+	status[frame] = size > cap ? ERRV(E_DST_TOO_SMALL) : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
+	if (needed)
+		needed[frame] = size;
+}
+
 template <int W, int PRE_P, int ENC_P, bool RICE_P, int ENC_S, bool RICE_S, int CH>
 __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 {
-	static_assert(CH % 2 == 0, "two register sets and two images alternate within a frame");
+	static_assert(CH % 2 == 0, "two images alternate within a frame");
 	constexpr uint32_t RW = EPT * W / 16u; // uint4 per lane
 	extern __shared__ __attribute__((aligned(16))) uint32_t L_img[];
 	__shared__ uint32_t s_wsum[2][CW_WAVES];
 	__shared__ __attribute__((aligned(16))) uint2 s_tab[2][WTAB];
 
 	const uint32_t tid = threadIdx.x, lane = tid & 63u;
-	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const uint32_t c = blockIdx.x;
 	const uint32_t n = a.n; // CH * CW_CHUNK
 	uint16_t *mbase = reinterpret_cast<uint16_t *>(a.model_ptrs ? (uint8_t *)(uintptr_t)a.model_ptrs[c]
@@ -620,7 +770,10 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 #pragma unroll
 	for (uint32_t d = 0; d < CW_DEPTH; d++)
 		pv[d] = 0u;
+	// unconditional loads (a step past the end reloads the last chunk): a
+	// conditional load into live registers makes the compiler wait for it
 	auto issue = [&](uint32_t set, uint32_t step) {
+		step = step < steps ? step : steps - 1u;
 		const uint32_t acq = step / CH, cc = step % CH;
 		const uint8_t *fs = a.src + (uint64_t)(c * a.fpc + acq) * a.src_stride;
 		const uint32_t first = cc * CW_CHUNK + tid * EPT;
@@ -628,9 +781,11 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 #pragma unroll
 		for (uint32_t q = 0; q < RW; q++)
 			rs[set][q] = p[q];
-		if (PRE_P == PRE_DIFF && lane == 0u && first != 0u)
-			pv[set] = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fs)[first - 1u]
-					 : reinterpret_cast<const uint32_t *>(fs)[first - 1u] & 0xFFFFu;
+		if (PRE_P == PRE_DIFF) {
+			const uint32_t ip = first ? first - 1u : 0u;
+			pv[set] = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fs)[ip]
+					 : reinterpret_cast<const uint32_t *>(fs)[ip];
+		}
 	};
 #pragma unroll
 	for (uint32_t d = 0; d < CW_DEPTH; d++)
@@ -641,7 +796,8 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 	const char *tab_p = reinterpret_cast<const char *>(s_tab[0]);
 	const char *tab_s = reinterpret_cast<const char *>(s_tab[1]);
 	uint32_t sq = seq0;
-	uint32_t used_prev = 0u; // image words the previous step used (cleared after its B1)
+	CwState st;
+	st.used_prev = 0u;
 	for (uint32_t acq = 0; acq < a.fpc; acq++) {
 		const uint32_t f = c * a.fpc + acq;
 		const bool prim = sq == 0u || sq > a.iters; // cmp.c:228-248
@@ -649,55 +805,25 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 		sq = prim ? 1u : sq + 1u;
 		const uint32_t HB = prim ? hdr_bits(PRE_P, ENC_P) : hdr_bits(PRE_MODEL, ENC_S);
 		const uint32_t enc = prim ? (uint32_t)ENC_P : (uint32_t)ENC_S;
-		// frame bit offset of the chunk, and the bits before it in its first word
-		uint32_t P = HB;
-		uint32_t carry = (HB & 31u) && enc != ENC_RAW ? ((prim ? cp.outlier : cs.outlier) & 0xFFFFu) << 16 : 0u;
+		// the frame's first payload word starts with header bytes 20-21
+		st.P = HB;
+		st.carry = (HB & 31u) && enc != ENC_RAW ? ((prim ? cp.outlier : cs.outlier) & 0xFFFFu) << 16 : 0u;
 		uint8_t *fdst = a.dst + (uint64_t)f * a.dst_stride;
-		const __amdgpu_buffer_rsrc_t dst_rsrc =
-			__builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(a.cap & ~3u), 0x00020000);
+		const u32x4 dst_rsrc = rsrc_words(fdst, a.cap & ~3u);
 #pragma unroll
 		for (uint32_t cc = 0; cc < CH; cc++) {
 			const uint32_t step = acq * CH + cc;
-			uint32_t *const img = (cc & 1u) ? img1 : img0;
-			uint32_t *const imgo = (cc & 1u) ? img0 : img1;
-			// ---- phase 1 -----------------------------------------------------
 			uint32_t w[EPT / 2];
-			if (W == 2) {
-#pragma unroll
-				for (uint32_t q = 0; q < RW; q++) {
-					w[4 * q] = rs[cc % CW_DEPTH][q].x ^ flip;
-					w[4 * q + 1] = rs[cc % CW_DEPTH][q].y ^ flip;
-					w[4 * q + 2] = rs[cc % CW_DEPTH][q].z ^ flip;
-					w[4 * q + 3] = rs[cc % CW_DEPTH][q].w ^ flip;
-				}
-			} else {
-#pragma unroll
-				for (uint32_t q = 0; q < RW; q++) {
-					w[2 * q] = __builtin_amdgcn_perm(rs[cc % CW_DEPTH][q].y, rs[cc % CW_DEPTH][q].x, 0x05040100u) ^ flip;
-					w[2 * q + 1] =
-						__builtin_amdgcn_perm(rs[cc % CW_DEPTH][q].w, rs[cc % CW_DEPTH][q].z, 0x05040100u) ^ flip;
-				}
-			}
-			const uint32_t prevs = pv[cc % CW_DEPTH];
-			if (step + CW_DEPTH < steps)
-				issue(cc % CW_DEPTH, step + CW_DEPTH); // lands while the chunks before it are coded
+			cw_pairs<W>(rs[cc % CW_DEPTH], flip, w);
+			const uint32_t prevs = (cc != 0u || tid >= 64u) ? pv[cc % CW_DEPTH] & 0xFFFFu : 0u;
+			issue(cc % CW_DEPTH, step + CW_DEPTH); // lands while the chunks before it are coded
 			uint32_t mp[EPT / 2], oq[EPT / 2];
 			uint32_t T;
 			if (prim) {
-				uint32_t wprev = 0u;
-				if (PRE_P == PRE_DIFF) {
-					wprev = __shfl_up(w[EPT / 2 - 1], 1, 64);
-					if (lane == 0u)
-						wprev = (prevs << 16) ^ flip;
-				}
+				cw_primary<PRE_P, ENC_P>(w, prevs, flip, lane, mp);
 #pragma unroll
-				for (uint32_t q = 0; q < EPT / 2; q++) {
-					uint32_t u = w[q] ^ flip;
-					if (PRE_P == PRE_DIFF)
-						u = unpk(pk(w[q]) - pk(__builtin_amdgcn_alignbit(w[q], q ? w[q - 1] : wprev, 16)));
-					mp[q] = ENC_P == ENC_RAW ? u : zigzag_pk(u);
+				for (uint32_t q = 0; q < EPT / 2; q++)
 					mdl[cc][q] = w[q]; // cmp.c:305-306
-				}
 				T = walk_lengths<ENC_P, RICE_P>(mp, oq, cp, fast_p, tab_p);
 			} else {
 				const int32_t r1 = 16 - (int32_t)a.model_rate;
@@ -712,66 +838,15 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 #pragma unroll
 			for (uint32_t q = 0; q < EPT / 2; q++)
 				asm volatile("" : "+v"(mp[q]), "+v"(oq[q]));
-			const uint32_t inc = wave_incl_scan(T);
-			if (lane == 63u)
-				s_wsum[cc & 1u][wid] = inc;
-			lds_barrier(); // B1: wave totals
-			// the previous chunk's image: stored, its carry taken; clear it
-			for (uint32_t i = tid; i < used_prev; i += CW_THREADS)
-				imgo[i] = 0u;
-			const uint32_t ws = lane < CW_WAVES ? s_wsum[cc & 1u][lane] : 0u;
-			const uint32_t wsc = wave_incl_scan(ws);
-			const uint32_t A = (uint32_t)__builtin_amdgcn_readlane((int)wsc, CW_WAVES - 1);
-			const uint32_t wex = wid ? (uint32_t)__builtin_amdgcn_readlane((int)wsc, (int)wid - 1) : 0u;
-			const uint32_t r = P & 31u;
-			// ---- pack at the chunk's frame bit offset mod 32 ---------------------
+			uint32_t *const img = (cc & 1u) ? img1 : img0;
+			uint32_t *const imgo = (cc & 1u) ? img0 : img1;
 			if (prim)
-				walk_pack<ENC_P, RICE_P>(img, r + wex + inc - T, mp, oq, cp, fast_p, tab_p);
+				cw_chunk<ENC_P, RICE_P>(st, img, imgo, s_wsum, cc & 1u, T, mp, oq, cp, fast_p, tab_p, dst_rsrc);
 			else
-				walk_pack<ENC_S, RICE_S>(img, r + wex + inc - T, mp, oq, cs, fast_s, tab_s);
-			if (tid == 0u && r)
-				__hip_atomic_fetch_or(reinterpret_cast<lds_u32 *>((uintptr_t)img), carry, __ATOMIC_RELAXED,
-						      __HIP_MEMORY_SCOPE_WORKGROUP);
-			lds_barrier(); // B2: the packed image
-			// ---- store the whole words, big-endian (frame word (P >> 5) + i) -----
-			const uint32_t end = r + A, nfull = end >> 5;
-			const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)img);
-			const uint32_t g0 = P >> 5;
-			for (uint32_t p = tid; p < (nfull >> 2); p += CW_THREADS) {
-				const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + 4u * p);
-				u32x4 o;
-				o.x = bswap32(wv.x);
-				o.y = bswap32(wv.y);
-				o.z = bswap32(wv.z);
-				o.w = bswap32(wv.w);
-				__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, (int)(4u * (g0 + 4u * p)), 0, 0);
-			}
-			const uint32_t rr = (tid - (nfull >> 2)) & (CW_THREADS - 1u);
-			if (rr < (nfull & 3u)) {
-				const uint32_t jw = (nfull & ~3u) + rr;
-				__builtin_amdgcn_raw_buffer_store_b32(bswap32(Ll[jw]), dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
-			}
-			carry = (end & 31u) ? __builtin_amdgcn_readfirstlane(Ll[nfull]) : 0u;
-			used_prev = nfull + 1u;
-			P += A;
+				cw_chunk<ENC_S, RICE_S>(st, img, imgo, s_wsum, cc & 1u, T, mp, oq, cs, fast_s, tab_s, dst_rsrc);
 		}
-		// ---- frame epilogue (cmp.c:314-334) -----------------------------------
 		if (tid == 0u) {
-			const uint32_t endbit = P;
-			if (endbit & 31u) { // zero-padded final bytes (bitstream_flush)
-				const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
-				for (uint32_t b = 0; b < nbytes; b++)
-					if (4u * (endbit >> 5) + b < a.cap)
-						fdst[4u * (endbit >> 5) + b] = (uint8_t)(carry >> (24u - 8u * b));
-			}
-			const uint32_t payload_bytes = (endbit + 7u) >> 3;
-			const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
-			if (a.checksum) {
-				const uint32_t ck = a.checksums[f];
-				for (uint32_t b = 0; b < 4u; b++)
-					if (payload_bytes + b < a.cap)
-						fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
-			}
+			const uint32_t size = ((st.P + 7u) >> 3) + (a.checksum ? 4u : 0u);
 			const uint64_t id = a.ids ? a.ids[f] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)acq * a.id_astep;
 			uint32_t h[5];
 			if (prim)
@@ -780,12 +855,8 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 			else
 				header_words(h, size, 2u * n, id, hseq, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S, a.model_rate,
 					     ENC_S == ENC_RAW ? 0u : cs.g, ENC_S == ENC_RAW ? 0u : cs.outlier);
-			const uint32_t hwords = HB == 176u ? 5u : 4u;
-			for (uint32_t wq = 0; wq < hwords; wq++)
-				if (4u * wq + 4u <= a.cap)
-					*reinterpret_cast<uint32_t *>(fdst + 4u * wq) = bswap32(h[wq]);
-			a.status[f] = size > a.cap ? ERRV(E_DST_TOO_SMALL)
-						   : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
+			cw_epilogue(fdst, a.cap, st.P, st.carry, HB, a.checksum != 0u, a.checksum ? a.checksums[f] : 0u, h,
+				    a.status, nullptr, f, size);
 		}
 	}
 	// the model after the last acquisition, to the work buffer (cmp.c:304-311)

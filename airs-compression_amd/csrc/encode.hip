@@ -1054,6 +1054,12 @@ static uint32_t image_words(uint32_t encoder_type, uint32_t g)
 	return (words + 3u) & ~3u;
 }
 
+// Rice ZERO or MULTI (g a power of two): the passes the walks code
+static bool walk_rice(uint32_t enc, uint32_t g)
+{
+	return (enc == ENC_ZERO || enc == ENC_MULTI) && g && (g & (g - 1u)) == 0u;
+}
+
 // Longest codeword (bits) a Rice pass emits with these parameters (the
 // outlier clamped as make_coder does); sizes the context walk's images
 static uint32_t code_max_bits(uint32_t enc, uint32_t g, uint32_t outlier_param)
@@ -1109,9 +1115,9 @@ static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t 
 			size_t lds = (size_t)2u * (k.img_words + 4u) * 4u; // two images (enc_kernel.h NIMG)
 			lds = lds > AUTO_BINS * 64u * 4u ? lds : AUTO_BINS * 64u * 4u; // the histogram
 			if (full)
-				launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, true, true>, k, grid, lds, s, false);
+				launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, true, true>, k, grid, lds, s);
 			else
-				launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, false, true>, k, grid, lds, s, false);
+				launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, false, true>, k, grid, lds, s);
 			return;
 		}
 	}
@@ -1122,14 +1128,14 @@ static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t 
 		return;
 	} else {
 		if (full)
-			launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, true>, k, grid, lds, s, true);
+			launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, true>, k, grid, lds, s);
 		return;
 	}
 #else
 	if (full)
-		launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, true>, k, grid, lds, s, true);
+		launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, true>, k, grid, lds, s);
 	else
-		launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, false>, k, grid, lds, s, true);
+		launch_segments(encode_kernel<W, PRE, ENC, RICE, MODEL, false>, k, grid, lds, s);
 #endif
 }
 
@@ -1407,10 +1413,6 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 }
 
 // ---- MODEL streams in one launch (enc_walk.hip) ----------------------------
-static bool walk_rice(uint32_t enc, uint32_t g)
-{
-	return (enc == ENC_ZERO || enc == ENC_MULTI) && g && (g & (g - 1u)) == 0u;
-}
 
 extern "C" int airs_dev_walk_supported(const struct airs_walk *w)
 {

@@ -518,8 +518,8 @@ def main():
         "cfg3": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO> (the per-frame Rice k chosen in-kernel): one "
                 "launch per step",
         "cfg4": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL>: one launch per step",
-        "cfg5": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice> (enc_walk.hip): ONE launch per step, every "
-                "acquisition of the 256 streams, the models kept on the chip",
+        "cfg5": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> (enc_walk.hip): ONE launch per step, one "
+                "1024-thread workgroup per stream walks its 16 acquisitions, the model in registers",
         "cfg5fb": "per acquisition: fb_step_kernel + fb_copy_kernel + encode_kernel<4,DIFF,ZERO,Rice,STORE> + "
                   "encode_kernel<4,MODEL,MULTI,Rice,UPDATE> (frame-list holes)",
     }
@@ -572,6 +572,11 @@ def main():
                 "algorithmic_bytes_note": "compulsory HBM reads of one step: 2 B/sample (u16), 4 B/sample "
                                           "(i16-in-i32), +2 B/sample model read per MODEL pass (SURVEY 8(d))",
                 "avg_launch_ms_hip_events": round(kern_avg_ms, 5),
+                **({"frac_samples_only": round(in_bytes_rank / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "frac_samples_only_note": "the same launches against the sample bytes alone (4 B/sample): "
+                                              "the model stays on the chip between acquisitions, so its 2 B/sample "
+                                              "per MODEL pass are not re-read from HBM"}
+                   if wl["params"].get("secondary_preprocessing") == MODEL else {}),
                 "avg_launch_note": "HIP events around the K back-to-back steps on the engine stream, / K "
                                    "(all launches of a step)",
             },

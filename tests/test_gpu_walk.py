@@ -255,3 +255,62 @@ def test_walk_ctx_vs_call_loop(prod, eng, orc, case):
         bad = [f for f in range(len(fw)) if fw[f] != fg[f]]
         assert not bad, f"call {ci}: frames {bad[:8]} differ"
         assert sw == sg, f"call {ci}: context states differ"
+
+
+FRAME_CASES = [  # (kind, pre, enc, g, outlier, checksum, frames)
+    ("u16", 1, 1, 32, 0, 0, 300),  # BASELINE configs 1/3's parameters; 300 frames: some workgroups code two
+    ("i16", 0, 2, 8, 107, 1, 256),
+    ("i16_in_i32", 1, 2, 4, 30, 0, 256),
+    ("u16", 0, 1, 1024, 0, 1, 257),
+]
+
+
+@pytest.mark.parametrize("case", range(len(FRAME_CASES)))
+def test_large_batches_64ki_vs_call_loop(prod, eng, orc, case):
+    """Batches of >= 256 frames of 64 Ki samples without a model (cfg4's
+    shape; a frame walk, one workgroup per frame, was measured slower than the
+    encode kernel here and is not built): frames, sizes and the context state
+    equal the call loop, identifiers included."""
+    kind, pre, enc, g, outl, ck, nfr = FRAME_CASES[case]
+    rng = np.random.default_rng(700 + case)
+    n = 65536
+    p = P(primary_preprocessing=pre, primary_encoder_type=enc, primary_encoder_param=g, primary_encoder_outlier=outl,
+          checksum_enabled=ck)
+    calls = [(nfr, make_frames(kind, n, nfr, rng))]
+    cap = 26 + 6 * n
+    want = run_host(orc, [p], kind, n, 1, calls, cap)
+    got = run_gpu(prod, eng, [p], kind, n, 1, calls, cap)
+    (fw, sw), (fg, sg) = want[0], got[0]
+    bad = [f for f in range(nfr) if fw[f] != fg[f]]
+    assert not bad, f"frames {bad[:8]} differ"
+    assert sw == sg
+
+
+UNIT_CASES = [  # (kind, pre, enc, g, outlier, checksum, units per frame, frames)
+    ("u16", 1, 1, 32, 0, 0, 16, 40),  # BASELINE config 1's parameters, 16-unit frames: look-back across steps
+    ("i16", 1, 1, 32, 0, 1, 3, 200),
+    ("i16_in_i32", 0, 2, 8, 107, 0, 1, 700),  # one-unit frames: no look-back, many steps
+    ("u16", 0, 2, 2, 60, 1, 5, 130),  # escapes longer than 32 bits
+    ("i16", 1, 1, 2048, 0, 0, 2, 300),  # k = 11: the longest table codes
+]
+
+
+@pytest.mark.parametrize("case", range(len(UNIT_CASES)))
+def test_whole_unit_frames_vs_call_loop(prod, eng, orc, case):
+    """Frames of whole 16384-sample units without a model, from one unit to
+    16 per frame, hundreds of frames (the look-back across many segments and
+    frames): frames, sizes and the context state equal the call loop,
+    identifiers included."""
+    kind, pre, enc, g, outl, ck, upf, nfr = UNIT_CASES[case]
+    rng = np.random.default_rng(900 + case)
+    n = 16384 * upf
+    p = P(primary_preprocessing=pre, primary_encoder_type=enc, primary_encoder_param=g, primary_encoder_outlier=outl,
+          checksum_enabled=ck)
+    calls = [(nfr, make_frames(kind, n, nfr, rng))]
+    cap = 26 + 6 * n
+    want = run_host(orc, [p], kind, n, 1, calls, cap)
+    got = run_gpu(prod, eng, [p], kind, n, 1, calls, cap)
+    (fw, sw), (fg, sg) = want[0], got[0]
+    bad = [f for f in range(nfr) if fw[f] != fg[f]]
+    assert not bad, f"frames {bad[:8]} differ"
+    assert sw == sg
