@@ -85,7 +85,9 @@ struct KArgs {
 // fused Rice selection: frames of at most AUTO_MAX_SPF segments (the frame's
 // 16 * spf candidate granules are read by one wave in AUTO_MAX_SPF / 4 loads
 // per lane); larger frames take select_rice_kernel first
+#ifndef AUTO_MAX_SPF
 #define AUTO_MAX_SPF 32u
+#endif
 // histogram bins: v = m + 1 in [1, 65536], bin = 8 floor(log2 v) + next 3 bits
 #define AUTO_BINS 129u
 

@@ -453,7 +453,7 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 				gran_store(&a.ktot[(uint64_t)gseg * 16u + lane], ((uint64_t)a.epoch << 32) | sk);
 			}
 			const uint32_t first_seg = gseg - sif, ng = a.segs_per_frame * 16u;
-			constexpr uint32_t NL = AUTO_MAX_SPF / 4u; // granule loads per lane
+			constexpr uint32_t NL = (AUTO_MAX_SPF + 3u) / 4u; // granule loads per lane
 			uint64_t gk[NL];
 #pragma unroll
 			for (uint32_t i = 0; i < NL; i++) {
