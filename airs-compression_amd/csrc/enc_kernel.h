@@ -374,6 +374,10 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 		__shared__ uint32_t s_hist[AUTO_BINS];
 		__shared__ uint32_t s_kt[EWG / 64][16];
 		uint32_t *const H = L_dyn;
+		// this lane's counter of bin b is at byte hbase + 256 (b + 1016): the
+		// bin's offset comes from the float bits with one bit-field extract
+		// and one shift-add (32-bit LDS address arithmetic wraps)
+		const uint32_t hbase = (uint32_t)(uintptr_t)H + 4u * lane - 1016u * 256u;
 		__syncthreads(); // the images are zeroed
 #pragma unroll
 		for (uint32_t c = 0; c < CH; c++) {
@@ -388,9 +392,13 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 					const uint32_t j = 2u * jp + h;
 					if ((FULL || j < nv[c]) && !AIRS_AUTO_ABL(1)) {
 						const uint32_t v = half16(wv, h) + 1u;
-						const uint32_t bin = (__float_as_uint((float)v) >> 20) - 1016u;
-						__hip_atomic_fetch_add(H + bin * 64u + lane, 1u, __ATOMIC_RELAXED,
-								       __HIP_MEMORY_SCOPE_WORKGROUP);
+						// (as asm: the compiler turns the pair into shift, and, add)
+						uint32_t ha;
+						asm("v_bfe_u32 %0, %1, 20, 12\n\tv_lshl_add_u32 %0, %0, 8, %2"
+						    : "=&v"(ha)
+						    : "v"(__float_as_uint((float)v)), "v"(hbase));
+						lds_u32 *hp = reinterpret_cast<lds_u32 *>((uintptr_t)ha);
+						__hip_atomic_fetch_add(hp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 					}
 				}
 			}
