@@ -51,7 +51,7 @@ struct airs_launch {
 	/* CMP_GPU_AUTO_RICE (GOLOMB_ZERO after NONE or DIFF): g = 2^k per frame by
 	 * the build-defined rule.  Frames of a few segments
 	 * choose k inside the encode kernel (one read of the samples); otherwise
-	 * select_rice_kernel writes g for the launch's frames into frame_g_scratch
+	 * the sliced Rice selection writes g for the launch's frames into frame_g_scratch
 	 * (device, one word per batch frame) first */
 	uint32_t auto_rice;
 	uint32_t *frame_g_scratch;

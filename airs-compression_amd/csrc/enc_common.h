@@ -84,7 +84,7 @@ struct KArgs {
 
 // fused Rice selection: frames of at most AUTO_MAX_SPF segments (the frame's
 // 16 * spf candidate granules are read by one wave in AUTO_MAX_SPF / 4 loads
-// per lane); larger frames take select_rice_kernel first
+// per lane); larger frames take the sliced selection (select_rice_hist_kernel) first
 #ifndef AUTO_MAX_SPF
 #define AUTO_MAX_SPF 32u
 #endif

@@ -618,13 +618,19 @@ __device__ __forceinline__ uint32_t key_term(uint32_t key, uint32_t k)
 	return top4 >> (k - (t - 3u)); // k in [t-3, t]
 }
 
+// Frames above AUTO_MAX_SPF segments (the fused path's limit), and MODEL
+// passes: the frame is split into slices of RICE_SLICE samples (a 4 Mi-sample
+// frame takes 128 workgroups).  Each slice builds its histogram in LDS and
+// adds the non-zero bins to the frame's global histogram (device atomics,
+// zeroed before the launch); select_rice_pick_kernel then takes the argmin of
+// the 16 totals, ties to the smaller k.
+#define RICE_SLICE (256u * AIRS_PT * 8u)
 template <int W, int PRE>
-__global__ __launch_bounds__(256) void select_rice_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
-							   const uint32_t *flist, uint32_t fadd, uint32_t fmul,
-							   uint32_t *out_g)
+__global__ __launch_bounds__(256) void select_rice_hist_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
+								const uint32_t *flist, uint32_t fadd, uint32_t fmul,
+								uint32_t *ghist)
 {
 	__shared__ uint32_t hist[4][128];
-	__shared__ uint64_t tot[16];
 	const uint32_t tid = threadIdx.x, wid = tid >> 6;
 	const uint32_t frame = flist ? flist[blockIdx.x] : fadd + blockIdx.x * fmul;
 	if (frame == AIRS_NO_FRAME)
@@ -633,7 +639,8 @@ __global__ __launch_bounds__(256) void select_rice_kernel(const uint8_t *src, ui
 	for (uint32_t i = tid; i < 4u * 128u; i += 256u)
 		(&hist[0][0])[i] = 0u;
 	__syncthreads();
-	for (uint32_t base = tid * AIRS_PT; base < n; base += 256u * AIRS_PT) {
+	const uint32_t s0 = blockIdx.y * RICE_SLICE, s1 = min(n, s0 + RICE_SLICE);
+	for (uint32_t base = s0 + tid * AIRS_PT; base < s1; base += 256u * AIRS_PT) {
 		uint32_t x[AIRS_PT];
 		load16<W>(f, base, n, x);
 		uint32_t prev = 0u;
@@ -650,13 +657,26 @@ __global__ __launch_bounds__(256) void select_rice_kernel(const uint8_t *src, ui
 		}
 	}
 	__syncthreads();
-	if (tid < 128u)
-		hist[0][tid] += hist[1][tid] + hist[2][tid] + hist[3][tid];
-	__syncthreads();
+	if (tid < 128u) {
+		const uint32_t c = hist[0][tid] + hist[1][tid] + hist[2][tid] + hist[3][tid];
+		if (c)
+			atomicAdd(&ghist[(uint64_t)blockIdx.x * 128u + tid], c);
+	}
+}
+
+__global__ __launch_bounds__(64) void select_rice_pick_kernel(uint32_t n, const uint32_t *flist, uint32_t fadd,
+							      uint32_t fmul, const uint32_t *ghist, uint32_t *out_g)
+{
+	__shared__ uint64_t tot[16];
+	const uint32_t tid = threadIdx.x;
+	const uint32_t frame = flist ? flist[blockIdx.x] : fadd + blockIdx.x * fmul;
+	if (frame == AIRS_NO_FRAME)
+		return;
+	const uint32_t *h = ghist + (uint64_t)blockIdx.x * 128u;
 	if (tid < 16u) {
 		uint64_t s = (uint64_t)n * (tid + 1u);
 		for (uint32_t key = 1; key < 128u; key++)
-			s += (uint64_t)hist[0][key] * key_term(key, tid);
+			s += (uint64_t)h[key] * key_term(key, tid);
 		tot[tid] = s;
 	}
 	__syncthreads();
@@ -956,6 +976,8 @@ struct airs_dev_engine {
 	size_t dbgts_n;
 	uint64_t *ktot; // fused Rice selection: 16 candidate granules per segment
 	size_t ktot_cap;
+	uint32_t *rhist; // sliced Rice selection: 128 bins per frame
+	size_t rhist_cap; // frames
 };
 
 extern "C" int airs_dev_available(void)
@@ -999,6 +1021,7 @@ extern "C" void airs_dev_engine_destroy(struct airs_dev_engine *e)
 	(void)hipFree(e->ticket);
 	(void)hipFree(e->dbgts);
 	(void)hipFree(e->ktot);
+	(void)hipFree(e->rhist);
 	for (int i = 0; i < AIRS_NSLOT; i++)
 		(void)hipFree(e->scratch[i]);
 	free(e);
@@ -1297,7 +1320,7 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	if (r)
 		return r;
 	// CMP_GPU_AUTO_RICE: fused into the encode kernel for frames of a few
-	// segments without a model; otherwise select_rice_kernel writes g first
+	// segments without a model; otherwise the sliced selection writes g first
 	const bool auto_fused = L->auto_rice && L->encoder_type == ENC_ZERO &&
 				L->model_mode == AIRS_MODEL_NONE &&
 				(L->preprocessing == PRE_NONE || L->preprocessing == PRE_DIFF) && spf <= AUTO_MAX_SPF;
@@ -1603,21 +1626,35 @@ extern "C" uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *
 	if (!e || !n || !num_frames)
 		return ERRV(E_GENERIC);
 	const uint8_t *s = (const uint8_t *)src;
+	if (num_frames > e->rhist_cap) {
+		HIPCHECK(hipStreamSynchronize(e->stream));
+		(void)hipFree(e->rhist);
+		e->rhist = nullptr;
+		e->rhist_cap = 0;
+		HIPCHECK(hipMalloc(&e->rhist, (size_t)num_frames * 128u * 4u));
+		e->rhist_cap = num_frames;
+	}
+	HIPCHECK(hipMemsetAsync(e->rhist, 0, (size_t)num_frames * 128u * 4u, e->stream));
+	const dim3 grid(num_frames, (n + RICE_SLICE - 1u) / RICE_SLICE);
+	if (grid.y > 65535u)
+		return ERRV(E_PARAMS_INVALID);
 	if (sample_bytes == 2) {
 		if (preprocessing == PRE_DIFF)
-			hipLaunchKernelGGL((select_rice_kernel<2, PRE_DIFF>), dim3(num_frames), dim3(256), 0,
-					   e->stream, s, src_stride, n, flist, fadd, fmul, out_g);
+			hipLaunchKernelGGL((select_rice_hist_kernel<2, PRE_DIFF>), grid, dim3(256), 0, e->stream, s, src_stride,
+					   n, flist, fadd, fmul, e->rhist);
 		else
-			hipLaunchKernelGGL((select_rice_kernel<2, PRE_NONE>), dim3(num_frames), dim3(256), 0,
-					   e->stream, s, src_stride, n, flist, fadd, fmul, out_g);
+			hipLaunchKernelGGL((select_rice_hist_kernel<2, PRE_NONE>), grid, dim3(256), 0, e->stream, s, src_stride,
+					   n, flist, fadd, fmul, e->rhist);
 	} else {
 		if (preprocessing == PRE_DIFF)
-			hipLaunchKernelGGL((select_rice_kernel<4, PRE_DIFF>), dim3(num_frames), dim3(256), 0,
-					   e->stream, s, src_stride, n, flist, fadd, fmul, out_g);
+			hipLaunchKernelGGL((select_rice_hist_kernel<4, PRE_DIFF>), grid, dim3(256), 0, e->stream, s, src_stride,
+					   n, flist, fadd, fmul, e->rhist);
 		else
-			hipLaunchKernelGGL((select_rice_kernel<4, PRE_NONE>), dim3(num_frames), dim3(256), 0,
-					   e->stream, s, src_stride, n, flist, fadd, fmul, out_g);
+			hipLaunchKernelGGL((select_rice_hist_kernel<4, PRE_NONE>), grid, dim3(256), 0, e->stream, s, src_stride,
+					   n, flist, fadd, fmul, e->rhist);
 	}
+	hipLaunchKernelGGL(select_rice_pick_kernel, dim3(num_frames), dim3(64), 0, e->stream, n, flist, fadd, fmul,
+			   (const uint32_t *)e->rhist, out_g);
 	HIPCHECK(hipGetLastError());
 	return 0;
 }

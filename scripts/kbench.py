@@ -41,7 +41,8 @@ src, dst = srcs[0], dsts[0]
 sizes = torch.zeros(nf, dtype=torch.int32, device="cuda")
 ctxs = pkg.context_array(1)
 lib.initialise(ctxs[0], api.CmpParams(**wl["params"]))
-flags = 1 if wl.get("auto_rice") else 0
+# AIRS_KB_AUTO=1: CMP_GPU_AUTO_RICE on any workload (no golden digest then)
+flags = 1 if (wl.get("auto_rice") or os.environ.get("AIRS_KB_AUTO")) else 0
 for k in range(10):
     assert eng.compress(ctxs, nf, "u16", src.data_ptr(), stride, stride, dst.data_ptr(), dstride, cap,
                         sizes.data_ptr(), flags) == 0
@@ -73,7 +74,7 @@ for j in range(nf):
 with open(os.path.join(bench.ROOT, "tests", "golden", "configs.json")) as f:
     gold = json.load(f)["configs"][wl["golden"]]
 want = gold["shard_digests_n1"][0] if wl["layout"] == "roundrobin" else gold["digest"]
-if os.environ.get("AIRS_KB_FRAMES"):
+if os.environ.get("AIRS_KB_FRAMES") or (os.environ.get("AIRS_KB_AUTO") and not wl.get("auto_rice")):
     want = None
 print(json.dumps(dict(workload=sys.argv[1], rot=ROT, dbg=os.environ.get("AIRS_DBG", "0"), median_ms=ms[len(ms) // 2],
                       min_ms=ms[0], GBps=round(nf * 2 * n / (ms[len(ms) // 2] * 1e-3) / 1e9, 1),

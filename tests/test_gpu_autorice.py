@@ -2,7 +2,7 @@
 against the oracle: k = orc_select_rice_k of the frame, then the oracle's
 GOLOMB_ZERO encoder with g = 2^k.  Frames of up to AUTO_MAX_SPF segments
 choose k inside the encode kernel (frame-major dispatch, 16 candidate granules
-per segment); larger frames go through select_rice_kernel first.  Both paths,
+per segment); larger frames go through the sliced selection first.  Both paths,
 both sample widths, NONE and DIFF, whole and partial segments, every k from 0
 to 15 (the scale of the noise sweeps it), and frames holding the extreme
 mapped value 65535 (v = 65536, the top histogram bin).  Bit-exact, with the
@@ -146,7 +146,7 @@ def test_autorice_k_range(prod, eng, orc, orc_ext):
 
 
 AUTO_BATCH = [  # (kind, n, fallback, flags beyond AUTO_RICE)
-    ("u16", AUTO_MAX_SPF * SEG16 + 100, 1, 0),  # device exact mode, select_rice_kernel per launch
+    ("u16", AUTO_MAX_SPF * SEG16 + 100, 1, 0),  # device exact mode, sliced selection per launch
     ("u16", AUTO_MAX_SPF * SEG16 + 100, 1, 0x2),  # the same, host-stepped
     ("i16_in_i32", 3 * SEG32 + 5, 1, 0),  # device exact mode, k chosen in the encode kernel
     ("i16", 2 * SEG16, 0, 0),  # asynchronous mode (one launch per acquisition step: no walk)
@@ -159,7 +159,7 @@ def test_autorice_model_batch(prod, eng, orc, orc_ext, kind, n, fallback, extra)
     primary (DIFF) passes take the per-frame g of the rule, the MODEL passes
     keep their configured g; contexts, models and fallbacks as the call loop
     with that g set before each call (identifiers included, unmasked).  Each
-    launch selects g for its own frames only (select_rice_kernel over the
+    launch selects g for its own frames only (the sliced selection over the
     launch's frame list)."""
     import batch_scenarios as bs
     rng = np.random.default_rng(n + extra)
