@@ -21,6 +21,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libairscmp.so")
 
 GPU_U16, GPU_I16, GPU_I16_IN_I32 = 0, 1, 2
 GPU_AUTO_RICE = 0x1
+REPORT_DRAWS = 0x8  # CMP_GPU_REPORT_DRAWS
 KIND_TO_GPU = {"u16": GPU_U16, "i16": GPU_I16, "i16_in_i32": GPU_I16_IN_I32}
 
 
@@ -147,6 +148,8 @@ class GpuEngine:
                  flags: int = 0, draws_ptr: int | None = None) -> int:
         """cmp_gpu_compress over device pointers; ctxs is a ctypes CmpContext array.
         draws_ptr: optional host uint8 array receiving each frame's identifier draws."""
+        if draws_ptr:
+            flags |= REPORT_DRAWS
         b = GpuBatch(type=KIND_TO_GPU[kind], src=src_ptr, src_stride=src_stride, src_size=src_size,
                      dst=dst_ptr, dst_stride=dst_stride, dst_capacity=dst_capacity,
                      sizes=sizes_ptr, flags=flags, draws=draws_ptr)

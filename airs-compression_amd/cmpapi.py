@@ -38,6 +38,7 @@ CMP_VERSION_NUMBER = 600
 GPU_AUTO_RICE = 0x1
 GPU_HOST_STEPPED = 0x2
 GPU_STEPWISE = 0x4
+GPU_REPORT_DRAWS = 0x8
 
 
 def err_value(name: str) -> int:

@@ -210,6 +210,10 @@ static int work_buf_state(const struct cmp_params *p)
 
 /* cmp_reset; with `draws` set the identifier draw is only counted (the batch
  * API draws the identifiers afterwards, in the reference's call order) */
+/* cmp_gpu_batch.draws is written only when the caller asks for it (ADVICE r3:
+ * a caller that fills the struct field by field may leave it uninitialised) */
+#define REPORT_DRAWS(b) (((b)->flags & CMP_GPU_REPORT_DRAWS) && (b)->draws)
+
 static uint32_t ctx_reset(struct cmp_context *ctx, uint32_t *draws)
 {
 	if (!ctx)
@@ -1014,7 +1018,7 @@ static uint32_t batch_exact(struct cmp_gpu_engine *eng, struct cmp_context *ctx,
 				for (k = 0; k < draws[f]; k++)
 					id = next_identifier();
 				ids[f] = id;
-				if (b->draws)
+				if (REPORT_DRAWS(b))
 					b->draws[f] = (uint8_t)draws[f];
 			}
 			ctx[c].identifier = id;
@@ -1277,7 +1281,7 @@ static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_contex
 			for (uint32_t k = 0; k < host_draws[f]; k++)
 				id = next_identifier();
 			ids[f] = id;
-			if (b->draws)
+			if (REPORT_DRAWS(b))
 				b->draws[f] = host_draws[f];
 		}
 		ctx[c].identifier = id;
@@ -1483,6 +1487,10 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		fprintf(stderr, "airscmp: cmp_gpu_compress: sizes array is NULL\n");
 		return ERRV(GENERIC);
 	}
+	if ((b->flags & CMP_GPU_REPORT_DRAWS) && !b->draws) {
+		fprintf(stderr, "airscmp: cmp_gpu_compress: CMP_GPU_REPORT_DRAWS without a draws array\n");
+		return ERRV(GENERIC);
+	}
 	if (!b->dst)
 		return ERRV(DST_NULL);
 	if (((uintptr_t)b->dst & 7u) || (b->dst_stride & 7u))
@@ -1580,7 +1588,7 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 					for (uint32_t k = 0; k < draws[f]; k++)
 						id = next_identifier();
 					plan[f].id = id;
-					if (b->draws)
+					if (REPORT_DRAWS(b))
 						b->draws[f] = (uint8_t)draws[f];
 				}
 				ctx[c].identifier = id;

@@ -1144,6 +1144,16 @@ static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t 
 			return;
 		}
 	}
+	// the arena kernel (enc_arena.hip): 16-bit NONE/DIFF, Rice ZERO with
+	// k <= 11 for every frame, no model, whole aligned segments
+	if constexpr (W == 2 && (PRE == PRE_NONE || PRE == PRE_DIFF) && ENC == ENC_ZERO && RICE && MODEL == 0) {
+		if (full && !k.frame_g && k.g >= 1u && k.g <= 2048u && arena_enabled()) {
+			KArgs ka = k;
+			ka.img_words = arena_words();
+			arena_encode(ka, PRE, false, grid, s);
+			return;
+		}
+	}
 	const size_t lds = (size_t)seg_images(W, MODEL) * (k.img_words + 4u) * 4u;
 #ifdef AIRS_EXP_ONLY
 	// experiment builds: only the benchmark kernels (u16/i16, DIFF, ZERO, Rice, FULL)

@@ -141,16 +141,36 @@ def pack(dst: torch.Tensor, dst_stride: int, sizes: torch.Tensor, num_frames: in
     return o[-1]
 
 
-def check_patchable(params, draws) -> None:
-    """Without per-frame draw counts every frame is taken to make one draw (a
-    primary pass that cannot fall back); raise ValueError unless `params`
-    guarantee that."""
-    if draws is not None:
+def check_patchable(params, draws, layout: str = "roundrobin") -> None:
+    """Raise ValueError unless the identifier patch of step 4 is exact.
+
+    Without per-frame draw counts every frame is taken to make one draw (a
+    primary pass that cannot fall back), which `params` must guarantee.  With
+    draw counts the fallback is fine (its extra draws are counted), but for
+    the frame layouts a frame must still not depend on the frame before it:
+    a secondary pass on one rank followed the previous frame of THAT rank's
+    context, not the previous global frame, so its identifier (and its bytes)
+    are not what one context over all frames would give.  So for
+    "roundrobin" and "block" secondary passes are refused, by the parameters
+    and by any frame that made no draw (a secondary pass draws nothing,
+    cmp.c:228-248).  "streams" keep every stream on one rank, so draws are
+    exact there."""
+    if draws is None:
+        if params is None or getattr(params, "secondary_iterations", 0) or \
+                getattr(params, "uncompressed_fallback_enabled", 0):
+            raise ValueError("identifier patching without per-frame draw counts needs secondary_iterations == 0 "
+                             "and the fallback disabled: pass the draws cmp_gpu_compress reports "
+                             "(cmp_gpu_batch.draws)")
         return
-    if params is None or getattr(params, "secondary_iterations", 0) or \
-            getattr(params, "uncompressed_fallback_enabled", 0):
-        raise ValueError("identifier patching without per-frame draw counts needs secondary_iterations == 0 "
-                         "and the fallback disabled: pass the draws cmp_gpu_compress reports (cmp_gpu_batch.draws)")
+    if layout == "streams":
+        return
+    if params is not None and getattr(params, "secondary_iterations", 0):
+        raise ValueError(f"identifier patching of the {layout!r} layout needs secondary_iterations == 0 (a "
+                         f"secondary pass depends on its rank's previous frame); use the 'streams' layout")
+    d = torch.as_tensor(draws)
+    if d.numel() and bool((d.reshape(-1) == 0).any()):
+        raise ValueError(f"identifier patching of the {layout!r} layout: a frame made no identifier draw (a "
+                         f"secondary pass, which depends on its rank's previous frame); use the 'streams' layout")
 
 
 def assign_identifiers(draws: torch.Tensor, base: int, layout: str, fpc: int = 1) -> tuple[torch.Tensor, torch.Tensor]:
@@ -201,7 +221,7 @@ class GatheredFrames:
         step 4), on the data's device.  Without gathered draw counts every
         frame counts one draw, which `params` must guarantee
         (check_patchable)."""
-        check_patchable(params, self.draws)
+        check_patchable(params, self.draws, self.layout)
         if self.num_frames == 0:
             return
         dev = self.data.device
@@ -296,7 +316,7 @@ def gather_frames_timed(dist, dst, dst_stride, sizes, num_frames, rank, world, r
     (stats dict, GatheredFrames or None)."""
     cuda = dst.is_cuda
     if patch_base is not None:
-        check_patchable(params, draws)  # on every rank, before any communication
+        check_patchable(params, draws, layout)  # on every rank, before any communication
 
     def sync():
         if cuda:

@@ -50,6 +50,9 @@ enum cmp_gpu_sample_type {
 #define CMP_GPU_STEPWISE 0x4u     /* MODEL contexts: one launch per acquisition step instead of
 				   * every acquisition in one launch with the models kept on
 				   * the chip; same output, for comparisons */
+#define CMP_GPU_REPORT_DRAWS 0x8u /* write each frame's identifier-draw count to batch->draws
+				   * (which must then be non-NULL); without it draws is never
+				   * touched */
 
 struct cmp_gpu_batch {
 	enum cmp_gpu_sample_type type;
@@ -61,11 +64,12 @@ struct cmp_gpu_batch {
 	uint32_t dst_capacity;  /* bytes available per frame */
 	uint32_t *sizes;        /* device [num frames]: frame size or error value */
 	uint32_t flags;
-	uint8_t *draws;         /* optional, HOST [num frames]: timestamp-callback draws each frame made
+	uint8_t *draws;         /* with CMP_GPU_REPORT_DRAWS, HOST [num frames]: timestamp-callback draws each frame made
 				 * (0: it carries its context's identifier; 1: a reset; 3 or 2: a
 				 * primary or secondary pass that fell back, cmp.c:342-393), for
 				 * assigning identifiers across processes (shard.py); valid when the
-				 * call returns */
+				 * call returns.  Zero-initialise the struct: fields added later
+				 * default to off */
 };
 
 struct cmp_gpu_engine;

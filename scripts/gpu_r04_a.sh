@@ -1,0 +1,9 @@
+# Round 4: GPU suite on the current tree, then an env A/B (scripts/gpu_envab.sh)
+#   VARIANTS=... WLS=... bash scripts/gpu_r04_a.sh TAG
+TAG=${1:-r04a}
+O=gpurun_out/$TAG
+cd "$GRAFT_REPO_ROOT" && mkdir -p $O && export TMPDIR=/tmp || exit 1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; tail -5 $O/pytest_gpu.log
+[ $rc -eq 0 ] || [ -n "$SKIP_TESTS_OK" ] || exit $rc
+bash scripts/gpu_envab.sh $TAG

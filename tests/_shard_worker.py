@@ -180,6 +180,20 @@ def run(rank, world, port, nf, n, layout, mode):
             else:
                 raise AssertionError("error value was not reported")
             return
+        if mode == "patch_refused_draws":
+            # draw counts replace only the fallback restriction: a frame layout
+            # with secondary passes is still refused (by the parameters, and by
+            # a frame that made no draw), on every rank before any communication
+            for prm, d in ((api.CmpParams(**PARAMS, secondary_iterations=2), torch.ones(nf, dtype=torch.uint8)),
+                           (None, torch.tensor([1] + [0] * (nf - 1), dtype=torch.uint8))):
+                try:
+                    shard.gather_frames_timed(dist, dst_t, stride, sizes_t, nf, rank, world, layout=layout,
+                                              patch_base=0, params=prm, draws=d)
+                except ValueError as e:
+                    assert "secondary" in str(e)
+                else:
+                    raise AssertionError("patching a frame layout with secondary passes was not refused")
+            return
         if mode == "patch_refused":
             try:
                 shard.gather_frames_timed(dist, dst_t, stride, sizes_t, nf, rank, world, layout=layout,

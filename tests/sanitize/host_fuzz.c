@@ -162,6 +162,8 @@ static void fuzz_batch(struct cmp_gpu_engine *eng)
 		  (pick(4) ? 0u : CMP_GPU_STEPWISE);
 	draws = pick(2) ? calloc(nf, 1) : NULL;
 	b.draws = draws;
+	if (draws)
+		b.flags |= CMP_GPU_REPORT_DRAWS;
 	if (ok) {
 		if (!cmp_is_error(cmp_gpu_compress(eng, ctx, nctx, fpc, &b))) {
 			n_batch_ok++;

@@ -119,6 +119,9 @@ for kind, seg in (("u16", SEG16), ("i16", SEG16), ("i16_in_i32", SEG32)):
         for n in (1, 7, 4096, seg - 1, seg, 3 * seg + 517, 4 * seg, AUTO_MAX_SPF * seg,
                   AUTO_MAX_SPF * seg + 100):
             CASES.append((kind, pre, n))
+# cfg2-shaped frames (4 Mi samples, 256 segments) and 1 Mi i16-in-i32 samples:
+# the sliced selection (one workgroup per 32 Ki-sample slice, not per frame)
+CASES += [("u16", 1, 4 << 20), ("i16", 0, 4 << 20), ("i16_in_i32", 1, 1 << 20)]
 
 
 @pytest.mark.parametrize("kind,pre,n", CASES)

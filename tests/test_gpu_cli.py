@@ -2,25 +2,48 @@
 test/cli_compression_test.py cases, frames checked byte for byte against the
 CPU oracle fed the same files through one context (header identifiers
 excepted: they come from the clock), and .air files decompressed back to the
-input samples."""
+input samples.
+
+Every compression case runs twice: on this build's airspace
+(airs-compression_amd/bin/airspace) and on the REFERENCE's own command-line
+tool, programs/airspacecli.c with its helpers compiled unchanged from the
+reference tree and linked to libairscmp.so only (tests/dropin/Makefile; built
+by __graft_entry__.build() where the reference is present): the literal
+drop-in of north_star ("drops in under programs/airspacecli").  The
+reference tool has no decompression (programs/airspacecli.c:421-423), so the
+round trips decode its .air output with this build's airspace."""
 import os
 import subprocess
 
 import numpy as np
 import pytest
 
-from conftest import PKG_DIR, load_pkg
+from conftest import PKG_DIR, ROOT, load_pkg
 
 pytestmark = pytest.mark.gpu
 CLI = os.path.join(PKG_DIR, "bin", "airspace")
+REF_CLI = os.path.join(ROOT, "tests", "dropin", "airspacecli")
 api = load_pkg().cmpapi
 DATA1 = bytes.fromhex("0001 0002")
 DATA2 = bytes.fromhex("0003 0004")
 HDR = 16  # NONE + UNCOMPRESSED header (the CLI's default parameters)
 
 
-def run(args, cwd, stdin=b""):
-    return subprocess.run([CLI] + [str(a) for a in args], input=stdin, capture_output=True, cwd=cwd, timeout=120)
+@pytest.fixture(params=["airspace", "reference"])
+def cli(request):
+    """The compressing tool under test: this build's CLI, or the reference's
+    airspacecli linked to libairscmp.so."""
+    if request.param == "airspace":
+        return CLI
+    if not os.path.exists(REF_CLI):
+        pytest.skip("tests/dropin/airspacecli not built (the reference tree was absent at build time)")
+    ldd = subprocess.run(["ldd", REF_CLI], capture_output=True, text=True).stdout
+    assert "libairscmp.so" in ldd, ldd  # the reference tool runs on this library
+    return REF_CLI
+
+
+def run(args, cwd, stdin=b"", tool=CLI):
+    return subprocess.run([tool] + [str(a) for a in args], input=stdin, capture_output=True, cwd=cwd, timeout=120)
 
 
 @pytest.fixture
@@ -39,94 +62,94 @@ def ok(r):
 
 
 # ---- cli_compression_test.py ------------------------------------------------
-def test_two_files_to_dev_null(files):
+def test_two_files_to_dev_null(cli, files):
     d, f1, f2 = files
-    r = ok(run(["-c", f1, f2, "-o", os.devnull, "--quiet"], d))
+    r = ok(run(["-c", f1, f2, "-o", os.devnull, "--quiet"], d, tool=cli))
     assert r.stderr == b""
 
 
-def test_two_files_to_stdout(files):
+def test_two_files_to_stdout(cli, files):
     d, f1, f2 = files
-    r = ok(run(["-c", f1, f2, "--stdout"], d))
+    r = ok(run(["-c", f1, f2, "--stdout"], d, tool=cli))
     assert r.stderr == b""
     assert r.stdout[HDR:HDR + 4] == DATA1 and r.stdout[2 * HDR + 4:] == DATA2
 
 
-def test_two_files_normally(files):
+def test_two_files_normally(cli, files):
     d, f1, f2 = files
-    r = ok(run(["-c", f1, f2, "--quiet"], d))
+    r = ok(run(["-c", f1, f2, "--quiet"], d, tool=cli))
     assert r.stderr == b""
     assert (d / "file_1.bin.air").read_bytes()[HDR:] == DATA1
     assert (d / "file_2.bin.air").read_bytes()[HDR:] == DATA2
 
 
 @pytest.mark.parametrize("arg", [["-"], []])
-def test_stdin_to_stdout(files, arg):
+def test_stdin_to_stdout(cli, files, arg):
     d, _, _ = files
-    r = ok(run(["-c"] + arg, d, stdin=DATA1))
+    r = ok(run(["-c"] + arg, d, stdin=DATA1, tool=cli))
     assert r.stdout[HDR:] == DATA1 and len(r.stdout) == HDR + 4
 
 
-def test_file_to_output_file(files):
+def test_file_to_output_file(cli, files):
     d, f1, _ = files
-    ok(run(["-c", f1, "-o", d / "output.air", "--quiet"], d))
+    ok(run(["-c", f1, "-o", d / "output.air", "--quiet"], d, tool=cli))
     assert (d / "output.air").read_bytes()[HDR:] == DATA1
 
 
-def test_file_and_stdin(files):
+def test_file_and_stdin(cli, files):
     d, f1, _ = files
-    r = ok(run(["-c", f1, "-", "--quiet"], d, stdin=DATA2))
+    r = ok(run(["-c", f1, "-", "--quiet"], d, stdin=DATA2, tool=cli))
     assert r.stdout[HDR:HDR + 4] == DATA1 and r.stdout[2 * HDR + 4:] == DATA2
 
 
-def test_files_of_different_sizes(files):
+def test_files_of_different_sizes(cli, files):
     d, f1, _ = files
     small = d / "small_file.bin"
     small.write_bytes(bytes.fromhex("0003"))
-    ok(run(["-c", f1, small, "--quiet"], d))
+    ok(run(["-c", f1, small, "--quiet"], d, tool=cli))
     assert (d / "file_1.bin.air").read_bytes()[HDR:] == DATA1
     assert (d / "small_file.bin.air").read_bytes()[HDR:] == bytes.fromhex("0003")
 
 
-def test_summary_line(files):
+def test_summary_line(cli, files):
     d, f1, f2 = files
-    r = ok(run(["-c", f1, f2], d))
+    r = ok(run(["-c", f1, f2], d, tool=cli))
     assert r.stderr.startswith(b"2 files compressed: ")
-    r = ok(run(["-c", d / "file_1.bin", "-o", d / "one.air"], d))
+    r = ok(run(["-c", d / "file_1.bin", "-o", d / "one.air"], d, tool=cli))
     assert b"file_1.bin: " in r.stderr and b"one.air" in r.stderr
 
 
-def test_not_overwrite_existing_file(files):
+def test_not_overwrite_existing_file(cli, files):
     d, f1, f2 = files
     existing = d / "existing_file.txt"
     existing.write_text("Do not overwrite this file!")
-    r = run(["-c", f1, f2, "-o", existing], d)
+    r = run(["-c", f1, f2, "-o", existing], d, tool=cli)
     assert r.returncode == 1 and b"already exists" in r.stderr
     assert existing.read_text() == "Do not overwrite this file!"
 
 
-def test_not_overwrite_existing_directory(files):
+def test_not_overwrite_existing_directory(cli, files):
     d, f1, f2 = files
     (d / "existing_dir").mkdir()
-    r = run(["-c", f1, f2, "-o", d / "existing_dir"], d)
+    r = run(["-c", f1, f2, "-o", d / "existing_dir"], d, tool=cli)
     assert r.returncode == 1 and b"is a directory" in r.stderr
 
 
-def test_not_overwrite_input_file(files):
+def test_not_overwrite_input_file(cli, files):
     d, f1, _ = files
-    r = run(["-c", f1, "-o", f1], d)
+    r = run(["-c", f1, "-o", f1], d, tool=cli)
     assert r.returncode == 1 and b"already exists" in r.stderr and f1.read_bytes() == DATA1
 
 
-def test_odd_sized_and_empty_files(files):
+def test_odd_sized_and_empty_files(cli, files):
     d, f1, _ = files
     odd, empty = d / "odd.bin", d / "empty.bin"
     odd.write_bytes(b"\x00\x01\x02")
     empty.write_bytes(b"")
-    r = run(["-c", f1, odd, "--quiet"], d)
+    r = run(["-c", f1, odd, "--quiet"], d, tool=cli)
     assert r.returncode == 1 and b"multiple of 2" in r.stderr
     assert (d / "file_1.bin.air").read_bytes()[HDR:] == DATA1  # files before the bad one are written
-    r = run(["-c", empty], d)
+    r = run(["-c", empty], d, tool=cli)
     assert r.returncode == 1 and b"is empty" in r.stderr
 
 
@@ -187,12 +210,12 @@ def masked(frame):
 
 
 @pytest.mark.parametrize("kind", list(PARAMS))
-def test_frames_match_oracle_and_decompress(tmp_path, prod, orc, kind):
+def test_frames_match_oracle_and_decompress(tmp_path, prod, orc, kind, cli):
     if not prod.gpu_available():
         pytest.fail("GPU test run without a usable HIP device")
     rng = np.random.default_rng(sum(map(ord, kind)))
     paths, xs = sample_files(tmp_path, kind, rng)
-    r = ok(run(["-c", "--params", params_arg(PARAMS[kind])] + paths + ["--stdout"], tmp_path))
+    r = ok(run(["-c", "--params", params_arg(PARAMS[kind])] + paths + ["--stdout"], tmp_path, tool=cli))
     frames = split_frames(r.stdout)
     assert len(frames) == len(xs)
 

@@ -42,6 +42,14 @@ def test_gather_world2_patch_refused_with_secondary_passes(orc):
     _spawn(3, 500, "roundrobin", "patch_refused")
 
 
+@pytest.mark.parametrize("layout", ["roundrobin", "block"])
+def test_gather_world2_patch_refused_with_draws_and_secondary_passes(orc, layout):
+    """per-frame draw counts do not make a frame layout with
+    secondary passes patchable (a secondary frame followed its rank's previous
+    frame); refused with and without the parameters at hand."""
+    _spawn(3, 500, layout, "patch_refused_draws")
+
+
 def test_gather_world2_fallback_identifiers_vs_one_context(orc):
     """Round-robin frames with the uncompressed fallback (three draws per
     fallback frame): after the gather every frame, identifier included, equals
