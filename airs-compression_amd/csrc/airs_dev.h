@@ -123,6 +123,16 @@ struct airs_walk {
 	uint32_t checksum_enabled;
 	const uint32_t *checksums; /* device [num_ctx * fpc] */
 	uint32_t *status;         /* device [num_ctx * fpc] */
+	/* uncompressed fallback on the chip (cmp.c:342-393; the context walk
+	 * only): cap is the raw frame size; a frame whose coded size exceeds it is
+	 * written raw (NONE + UNCOMPRESSED, sequence number 0), the model takes its
+	 * samples and the context continues at sequence number 1.  The identifier
+	 * draws of every frame (1 per reset: 0/1, 3 or 2 with a fallback) and the
+	 * final sequence numbers are written for the host, which draws the
+	 * identifiers in call order and patches the headers. */
+	uint32_t fb, raw_size;
+	uint8_t *draws;           /* device [num_ctx * fpc], with fb */
+	uint8_t *seq_out;         /* device [num_ctx], with fb */
 };
 int airs_dev_walk_supported(const struct airs_walk *w);
 uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_walk *w);

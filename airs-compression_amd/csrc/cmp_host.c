@@ -1463,6 +1463,176 @@ static uint32_t batch_walk(struct cmp_gpu_engine *eng, const struct cmp_context 
 	return airs_dev_walk(dev, &w);
 }
 
+/*
+ * MODEL contexts with the uncompressed fallback in one launch (the context
+ * walk, enc_walk.hip): the walk resolves each frame's fallback on the chip
+ * (cmp.c:342-393) and reports every frame's identifier draws and each
+ * context's final sequence number; one read-back, then the identifiers are
+ * drawn in call order and patched into the headers, as batch_device_exact
+ * does.  Applies when the fallback is the only way a frame's outcome can
+ * change the next frame's pass: every context with the same parameters, the
+ * fallback enabled and dst_capacity >= the raw frame size (the first
+ * attempt's capacity is then the raw size, so a frame either fits or falls
+ * back), and no secondary first frame whose model size differs (no
+ * SRC_SIZE_MISMATCH).  Returns 0, an error value, or WALK_NO.
+ */
+static uint32_t batch_walk_fb(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx, uint32_t fpc,
+			      const struct cmp_gpu_batch *b, uint64_t *ids)
+{
+	struct airs_dev_engine *dev = eng->dev;
+	const struct cmp_params *P = &ctx[0].params;
+	const uint32_t bytes = b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
+	const uint32_t n = b->src_size / bytes, total = num_ctx * fpc;
+	const uint32_t raw = raw_frame_size(&ctx[0], n);
+	const size_t tb = ((size_t)total + 15u) & ~(size_t)15u;
+	struct airs_walk w;
+	uint32_t c, a, e = 0, seq_same = 1, m_strided = 1;
+	uint64_t mbase, mstep;
+	uint8_t *h_draws = NULL, *h_seq = NULL, *scr;
+
+	if (!model_needed(P) || !P->uncompressed_fallback_enabled || b->dst_capacity < raw || raw > 0xFFFFFFu ||
+	    (P->primary_preprocessing != CMP_PREPROCESS_NONE && P->primary_preprocessing != CMP_PREPROCESS_DIFF))
+		return WALK_NO;
+	if ((b->flags & CMP_GPU_AUTO_RICE) && P->primary_encoder_type == CMP_ENCODER_GOLOMB_ZERO)
+		return WALK_NO;
+	for (c = 0; c < num_ctx; c++) {
+		const uint32_t sq = ctx[c].sequence_number;
+
+		if (!same_params(&ctx[c].params, P))
+			return WALK_NO;
+		if (sq != 0u && sq <= P->secondary_iterations && ctx[c].model_size != 2u * n)
+			return WALK_NO; /* the reference returns SRC_SIZE_MISMATCH for that frame */
+		if (sq != ctx[0].sequence_number)
+			seq_same = 0;
+	}
+	memset(&w, 0, sizeof(w));
+	w.src = b->src;
+	w.src_stride = b->src_stride;
+	w.sample_bytes = bytes;
+	w.is_unsigned = b->type == CMP_GPU_U16;
+	w.n = n;
+	w.num_ctx = num_ctx;
+	w.fpc = fpc;
+	w.dst = b->dst;
+	w.dst_stride = b->dst_stride;
+	w.cap = raw; /* the first attempt's capacity (cmp.c:358-366) */
+	w.pre_p = P->primary_preprocessing;
+	w.enc_p = P->primary_encoder_type;
+	w.g_p = P->primary_encoder_param;
+	w.outl_p = P->primary_encoder_outlier;
+	w.enc_s = P->secondary_encoder_type;
+	w.g_s = P->secondary_encoder_param;
+	w.outl_s = P->secondary_encoder_outlier;
+	w.model_rate = P->model_rate;
+	w.iters = P->secondary_iterations;
+	w.checksum_enabled = P->checksum_enabled ? 1u : 0u;
+	w.status = b->sizes;
+	w.seq0 = ctx[0].sequence_number;
+	w.fb = 1;
+	w.raw_size = raw;
+	mbase = (uint64_t)(uintptr_t)ctx[0].work_buf;
+	mstep = num_ctx > 1 ? (uint64_t)(uintptr_t)ctx[1].work_buf - mbase : 0;
+	for (c = 0; c < num_ctx && m_strided; c++)
+		m_strided = (uint64_t)(uintptr_t)ctx[c].work_buf == mbase + c * mstep;
+	if (!m_strided)
+		for (c = 0; c < num_ctx; c++)
+			if ((uintptr_t)ctx[c].work_buf & 15u)
+				return WALK_NO;
+	w.model = (void *)(uintptr_t)mbase;
+	w.model_stride = m_strided ? mstep : 0;
+	/* scratch: draws [tb], final sequence numbers [num_ctx], first sequence numbers [num_ctx] */
+	scr = airs_dev_scratch(dev, SLOT_FL, tb + 2u * (size_t)num_ctx + 16u);
+	if (!scr)
+		return ERRV(GENERIC);
+	w.draws = scr;
+	w.seq_out = scr + tb;
+	{
+		struct airs_walk chk = w;
+
+		if (!m_strided)
+			chk.model = NULL, chk.model_stride = 0;
+		if (!airs_dev_walk_supported(&chk))
+			return WALK_NO;
+	}
+	h_draws = malloc(total);
+	h_seq = malloc(num_ctx);
+	if (!h_draws || !h_seq) {
+		e = ERRV(GENERIC);
+		goto out;
+	}
+	if (!m_strided) {
+		uint64_t *hp = malloc((size_t)num_ctx * 8u), *d_ptr = airs_dev_scratch(dev, SLOT_AUX, (size_t)num_ctx * 8u);
+
+		if (!hp || !d_ptr)
+			e = ERRV(GENERIC);
+		for (c = 0; c < num_ctx && !is_err(e); c++)
+			hp[c] = (uint64_t)(uintptr_t)ctx[c].work_buf;
+		if (!is_err(e))
+			e = airs_dev_h2d(dev, d_ptr, hp, (size_t)num_ctx * 8u);
+		if (!is_err(e))
+			e = airs_dev_sync(dev);
+		free(hp);
+		w.model_ptrs = d_ptr;
+	}
+	if (!seq_same && !is_err(e)) {
+		uint8_t *d_seq = scr + tb + num_ctx;
+
+		for (c = 0; c < num_ctx; c++)
+			h_seq[c] = ctx[c].sequence_number;
+		e = airs_dev_h2d(dev, d_seq, h_seq, num_ctx);
+		if (!is_err(e))
+			e = airs_dev_sync(dev);
+		w.seq0s = d_seq;
+	}
+	if (!is_err(e) && P->checksum_enabled) {
+		uint32_t *d_ck = airs_dev_scratch(dev, SLOT_CK, (size_t)total * 4u);
+
+		e = d_ck ? airs_dev_checksum(dev, b->src, b->src_stride, bytes, n, total, NULL, d_ck) : ERRV(GENERIC);
+		w.checksums = d_ck;
+	}
+	if (!is_err(e))
+		e = airs_dev_walk(dev, &w);
+	/* the one read-back: identifier draws and the final sequence numbers */
+	if (!is_err(e))
+		e = airs_dev_d2h(dev, h_draws, w.draws, total);
+	if (!is_err(e))
+		e = airs_dev_d2h(dev, h_seq, w.seq_out, num_ctx);
+	if (!is_err(e))
+		e = airs_dev_sync(dev);
+	if (is_err(e))
+		goto out;
+	for (c = 0; c < num_ctx; c++) {
+		uint64_t id = ctx[c].identifier;
+
+		for (a = 0; a < fpc; a++) {
+			const uint32_t f = c * fpc + a;
+
+			for (uint32_t k = 0; k < h_draws[f]; k++)
+				id = next_identifier();
+			ids[f] = id;
+			if (REPORT_DRAWS(b))
+				b->draws[f] = h_draws[f];
+		}
+		ctx[c].identifier = id;
+		ctx[c].sequence_number = h_seq[c];
+		ctx[c].model_size = 2u * n; /* every context's model holds a frame of this size */
+	}
+	{
+		uint64_t *d_ids = airs_dev_scratch(dev, SLOT_IDS, (size_t)total * 8u);
+
+		if (!d_ids || is_err(airs_dev_h2d(dev, d_ids, ids, (size_t)total * 8u)))
+			e = ERRV(GENERIC);
+		else
+			e = airs_dev_patch_ids(dev, b->dst, b->dst_stride, total, 0, 1, d_ids, b->sizes);
+		if (!is_err(e))
+			e = airs_dev_sync(dev);
+	}
+out:
+	free(h_draws);
+	free(h_seq);
+	return e;
+}
+
 uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx,
 			  uint32_t fpc, const struct cmp_gpu_batch *b)
 {
@@ -1601,7 +1771,10 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		struct pass pp, ps;
 
 		memset(&ps, 0, sizeof(ps));
-		if (!(b->flags & CMP_GPU_HOST_STEPPED) && device_exact_ok(ctx, num_ctx, b, n, &pp, &ps))
+		if (!(b->flags & (CMP_GPU_HOST_STEPPED | CMP_GPU_STEPWISE)) && device_exact_ok(ctx, num_ctx, b, n, &pp, &ps) &&
+		    (e = batch_walk_fb(eng, ctx, num_ctx, fpc, b, ids)) != WALK_NO)
+			; /* MODEL contexts with the fallback: every acquisition in one launch (or an error) */
+		else if (!(b->flags & CMP_GPU_HOST_STEPPED) && device_exact_ok(ctx, num_ctx, b, n, &pp, &ps))
 			e = batch_device_exact(eng, ctx, num_ctx, fpc, b, &pp, &ps, ids);
 		else
 			e = batch_exact(eng, ctx, num_ctx, fpc, b, plan, ids, ptrs);

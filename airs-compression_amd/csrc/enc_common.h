@@ -22,6 +22,8 @@
 #define AIRS_SPIN_LIMIT (1u << 22)
 // engine->ticket[AIRS_FAULT_WORD] counts look-back give-ups (must stay 0)
 #define AIRS_FAULT_WORD 16
+// engine->ticket[AIRS_WALK_TICKET]: the segment walk's logical block tickets
+#define AIRS_WALK_TICKET 32
 
 // Ablation switches (AIRS_DBG bits, benchmarking only) are compiled in only
 // with -DAIRS_ABLATE=1: in the product build every DBG() is a constant false,
@@ -470,6 +472,10 @@ struct WArgs {
 	uint32_t cap, iters, seq0, epoch;
 	uint32_t g_p, outl_p, g_s, outl_s;
 	uint32_t model_rate, is_unsigned, checksum, img_words;
+	uint32_t fb, raw_size; // uncompressed fallback on the chip (walk_ctx_kernel, airs_walk)
+	uint32_t ticket_base;  // walk_kernel: ticket[AIRS_WALK_TICKET] before the launch
+	uint8_t *draws;        // identifier draws per frame (fb)
+	uint8_t *seq_out;      // sequence number per context after the walk (fb)
 	uint32_t dbg;    // ablation builds: AIRS_DBG switches (0 in production)
 	uint64_t *dbgts; // AIRS_DBG bit 65536: 8 realtime stamps per (workgroup, acquisition)
 };

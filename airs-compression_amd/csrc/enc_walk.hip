@@ -257,13 +257,24 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 	const uint32_t tid = threadIdx.x, lane = tid & 63u;
 	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const bool data = wid < 4u;
-	const uint32_t c = blockIdx.x / a.spf, j = blockIdx.x - c * a.spf;
+	// logical block index from a ticket taken at start: every
+	// workgroup with a smaller index has started (is resident or done), so a
+	// look-back only ever waits on a workgroup that is running, whatever order
+	// the XCDs dispatch in
+	if (tid == 0u)
+		s_ctl[3] = atomicAdd(a.ticket + AIRS_WALK_TICKET, 1u) - a.ticket_base;
+	__syncthreads();
+	const uint32_t lb = __builtin_amdgcn_readfirstlane(s_ctl[3]);
+	const uint32_t c = lb / a.spf, j = lb - c * a.spf;
 	const bool is_first = j == 0u, is_last = j + 1u == a.spf;
 	const uint32_t n = a.n;
 	const uint32_t first = j * AIRS_SEG + (data ? tid : 0u) * EPT; // lane's first sample
 	uint16_t *mbase = reinterpret_cast<uint16_t *>(a.model_ptrs ? (uint8_t *)(uintptr_t)a.model_ptrs[c]
 								    : a.model + (uint64_t)c * a.model_stride);
-	uint32_t *img = L_img + 4u;
+	// two images (a.img_words each, after a 4-word pad): acquisition a packs
+	// into image a % 2 and is stored in the next step, once its frame offset
+	// is known
+	uint32_t *const img0 = L_img + 4u, *const img1 = L_img + 8u + a.img_words;
 
 	const Coder cp = make_coder<ENC_P>(ENC_P == ENC_RAW ? 1u : a.g_p, a.outl_p);
 	const Coder cs = make_coder<ENC_S>(ENC_S == ENC_RAW ? 1u : a.g_s, a.outl_s);
@@ -275,7 +286,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		if (fast_s)
 			s_tab[1][tid] = walk_table_entry<ENC_S>(tid, cs);
 	}
-	for (uint32_t i = tid; i < a.img_words + 4u; i += 320u)
+	for (uint32_t i = tid; i < 2u * a.img_words + 8u; i += 320u)
 		L_img[i] = 0u;
 
 	const uint32_t seq0 = a.seq0s ? a.seq0s[c] : a.seq0;
@@ -315,21 +326,32 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 	};
 	if (data)
 		issue(0u);
-	__syncthreads(); // tables and the zeroed image
+	__syncthreads(); // tables and the zeroed images
 
 	const char *tab_p = reinterpret_cast<const char *>(s_tab[0]);
 	const char *tab_s = reinterpret_cast<const char *>(s_tab[1]);
 	uint32_t sq = seq0;
-	for (uint32_t acq = 0; acq < a.fpc; acq++) {
+	// the previous acquisition (packed, waiting for its frame offset)
+	uint32_t A_prev = 0u, HB_prev = 0u, hseq_prev = 0u;
+	bool prim_prev = false;
+	// Step `acq` codes acquisition acq (acq < fpc) and stores acquisition
+	// acq - 1 (acq > 0).  The look-back of acquisition acq - 1 runs in step acq:
+	// every segment published its aggregate for it one step earlier, so it is
+	// one granule round trip, overlapped with this step's packing, and never
+	// waits on a chain of predecessors.
+	for (uint32_t acq = 0; acq <= a.fpc; acq++) {
+		const bool have = acq < a.fpc, prev = acq > 0u;
 		const uint32_t f = c * a.fpc + acq;
 		const bool prim = sq == 0u || sq > a.iters; // cmp.c:228-248
 		const uint32_t hseq = prim ? 0u : sq;
-		sq = prim ? 1u : sq + 1u;
+		if (have)
+			sq = prim ? 1u : sq + 1u;
 		const uint32_t HB = prim ? hdr_bits(PRE_P, ENC_P) : hdr_bits(PRE_MODEL, ENC_S);
-		const uint32_t gseg = f * a.spf + j;
+		uint32_t *const img = (acq & 1u) ? img1 : img0;
+		uint32_t *const imgp = (acq & 1u) ? img0 : img1;
 		uint32_t mp[EPT / 2], oq[EPT / 2];
 		uint32_t T = 0u, excl = 0u;
-		if (data) {
+		if (have && data) {
 			// ---- phase 1: samples, residuals, model update, lengths ----------
 			uint32_t w[EPT / 2];
 			if (W == 2) {
@@ -388,167 +410,179 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		}
 		lds_barrier(); // B1: wave totals
 		const uint32_t w0 = s_wsum[0], w1 = s_wsum[1], w2 = s_wsum[2], w3 = s_wsum[3];
-		const uint32_t A = __builtin_amdgcn_readfirstlane(w0 + w1 + w2 + w3);
+		const uint32_t A = have ? __builtin_amdgcn_readfirstlane(w0 + w1 + w2 + w3) : 0u;
 		if (wid == 0u)
-			wstamp(a, acq, 1u);
+			wstamp(a, acq < a.fpc ? acq : a.fpc - 1u, 1u);
 		if (data) {
-			excl += (wid > 0u ? w0 : 0u) + (wid > 1u ? w1 : 0u) + (wid > 2u ? w2 : 0u);
-			// ---- pack into the image ----------------------------------------
-			if (prim)
-				walk_pack<ENC_P, RICE_P>(img, excl, mp, oq, cp, fast_p, tab_p);
-			else
-				walk_pack<ENC_S, RICE_S>(img, excl, mp, oq, cs, fast_s, tab_s);
-			if (wid == 3u && !is_last) {
-				// the segment's last 32 bits (wave 3's own lanes wrote them) for
-				// the successor's first word
-				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-				const uint32_t s0 = A - 32u, qw = s0 >> 5, sh = s0 & 31u;
-				const uint32_t tl = sh ? (img[qw] << sh) | (img[qw + 1u] >> (32u - sh)) : img[qw];
-				if (lane == 0u)
-					gran_store(&a.tail[gseg], ((uint64_t)a.epoch << 32) | tl);
+			if (have) {
+				excl += (wid > 0u ? w0 : 0u) + (wid > 1u ? w1 : 0u) + (wid > 2u ? w2 : 0u);
+				// ---- pack into this acquisition's image -------------------------
+				if (prim)
+					walk_pack<ENC_P, RICE_P>(img, excl, mp, oq, cp, fast_p, tab_p);
+				else
+					walk_pack<ENC_S, RICE_S>(img, excl, mp, oq, cs, fast_s, tab_s);
+				if (wid == 3u && !is_last) {
+					// the segment's last 32 bits (wave 3's own lanes wrote them) for
+					// the successor's first word (read by it one step later)
+					asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+					const uint32_t s0 = A - 32u, qw = s0 >> 5, sh = s0 & 31u;
+					const uint32_t tl = sh ? (img[qw] << sh) | (img[qw + 1u] >> (32u - sh)) : img[qw];
+					if (lane == 0u)
+						gran_store(&a.tail[(uint64_t)f * a.spf + j], ((uint64_t)a.epoch << 32) | tl);
+				}
 			}
 		} else {
-			// ---- control wave: aggregate, look-back, predecessor tail --------
-			if (lane == 0u) {
+			// ---- control wave: this step's aggregate, the previous step's
+			// look-back and predecessor tail ---------------------------------
+			if (have && lane == 0u) {
 				const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
-				gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HB + A : A));
+				gran_store(&a.agg[(uint64_t)f * a.spf + j], (tag << 32) | (is_first ? HB + A : A));
 			}
-			uint32_t P = HB, pred = 0u;
-			if (is_first) {
-				const uint32_t enc = prim ? ENC_P : ENC_S;
-				pred = (enc != ENC_RAW) ? ((prim ? cp.outlier : cs.outlier) & 0xFFFFu) : 0u;
-			} else {
-				const uint32_t first_seg = gseg - j;
-				uint32_t sum = 0u, spins = 0u;
-				int64_t jj = (int64_t)gseg - 1;
-				for (;;) {
-					const int64_t idx = jj - (int64_t)lane;
-					const bool inr = idx >= (int64_t)first_seg;
-					const uint64_t gv = inr ? gran_load(&a.agg[idx]) : 0ull;
-					const uint32_t tag = (uint32_t)(gv >> 32);
-					const bool valid = inr && (tag >> 1) == a.epoch;
-					const bool incl = valid && (tag & 1u);
-					const uint64_t incl_m = __ballot(incl);
-					const uint64_t bad_m = __ballot(inr && !valid);
-					const uint32_t fi = incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
-					const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
-					if (bad_m & need) { // a needed predecessor has not published yet
-						if (++spins > AIRS_SPIN_LIMIT) {
-							if (lane == 0)
+			if (prev) {
+				const uint64_t gseg = (uint64_t)(f - 1u) * a.spf + j;
+				uint32_t P = HB_prev, pred = 0u;
+				if (is_first) {
+					const uint32_t enc = prim_prev ? ENC_P : ENC_S;
+					pred = (enc != ENC_RAW) ? ((prim_prev ? cp.outlier : cs.outlier) & 0xFFFFu) : 0u;
+				} else {
+					const uint64_t first_seg = gseg - j;
+					uint32_t sum = 0u, spins = 0u;
+					int64_t jj = (int64_t)gseg - 1;
+					for (;;) {
+						const int64_t idx = jj - (int64_t)lane;
+						const bool inr = idx >= (int64_t)first_seg;
+						const uint64_t gv = inr ? gran_load(&a.agg[idx]) : 0ull;
+						const uint32_t tag = (uint32_t)(gv >> 32);
+						const bool valid = inr && (tag >> 1) == a.epoch;
+						const bool incl = valid && (tag & 1u);
+						const uint64_t incl_m = __ballot(incl);
+						const uint64_t bad_m = __ballot(inr && !valid);
+						const uint32_t fi = incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
+						const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
+						if (bad_m & need) { // a needed predecessor has not published yet
+							if (++spins > AIRS_SPIN_LIMIT) {
+								if (lane == 0)
+									atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+								break;
+							}
+							__builtin_amdgcn_s_sleep(1);
+							continue;
+						}
+						sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv : 0u);
+						if (incl_m)
+							break;
+						jj -= 64;
+					}
+					P = sum;
+					if (lane == 0u)
+						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (P + A_prev));
+					wstamp(a, acq - 1u, 5u);
+					// the predecessor's last 32 bits (published after its packing)
+					uint64_t tv = 0ull;
+					if (lane == 0u) {
+						uint32_t sp = 0u;
+						for (tv = gran_load(&a.tail[gseg - 1u]); (uint32_t)(tv >> 32) != a.epoch;
+						     tv = gran_load(&a.tail[gseg - 1u])) {
+							if (++sp > AIRS_SPIN_LIMIT) {
 								atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-							break;
+								break;
+							}
+							__builtin_amdgcn_s_sleep(1);
 						}
-						__builtin_amdgcn_s_sleep(1);
-						continue;
 					}
-					sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv : 0u);
-					if (incl_m)
-						break;
-					jj -= 64;
+					pred = (uint32_t)__shfl(tv, 0, 64);
+					wstamp(a, acq - 1u, 6u);
 				}
-				P = sum;
-				if (lane == 0u)
-					gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (P + A));
-				wstamp(a, acq, 5u);
-				// the predecessor's last 32 bits (published after its packing)
-				uint64_t tv = 0ull;
 				if (lane == 0u) {
-					uint32_t sp = 0u;
-					for (tv = gran_load(&a.tail[gseg - 1u]); (uint32_t)(tv >> 32) != a.epoch;
-					     tv = gran_load(&a.tail[gseg - 1u])) {
-						if (++sp > AIRS_SPIN_LIMIT) {
-							atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-							break;
-						}
-						__builtin_amdgcn_s_sleep(1);
-					}
+					s_ctl[0] = P;
+					s_ctl[1] = pred;
 				}
-				pred = (uint32_t)__shfl(tv, 0, 64);
-				wstamp(a, acq, 6u);
-			}
-			if (lane == 0u) {
-				s_ctl[0] = P;
-				s_ctl[1] = pred;
 			}
 		}
-		if (wid == 0u)
+		if (wid == 0u && have)
 			wstamp(a, acq, 2u);
-		lds_barrier(); // B2: packed image, offset and predecessor bits
-		if (wid == 0u)
-			wstamp(a, acq, 3u);
-		const uint32_t P = __builtin_amdgcn_readfirstlane(s_ctl[0]);
-		const uint32_t pred = __builtin_amdgcn_readfirstlane(s_ctl[1]);
-		const uint32_t r = P & 31u, g0 = P >> 5;
-		const uint32_t endbit = P + A;
-		const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
-		const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
-		uint8_t *fdst = a.dst + (uint64_t)f * a.dst_stride;
-		const __amdgpu_buffer_rsrc_t dst_rsrc =
-			__builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(a.cap & ~3u), 0x00020000);
-		if (data) {
-			// ---- store: funnel shift to the frame bit offset, big-endian ------
-			const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)img);
-			const uint32_t nquad = nfull >> 2;
-			for (uint32_t p = tid; p < nquad; p += 256u) {
-				const uint32_t jw = 4u * p;
-				const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + jw);
-				const uint32_t hi = jw ? Ll[jw - 1u] : pred;
-				u32x4 o;
-				o.x = bswap32(__builtin_amdgcn_alignbit(hi, wv.x, r));
-				o.y = bswap32(__builtin_amdgcn_alignbit(wv.x, wv.y, r));
-				o.z = bswap32(__builtin_amdgcn_alignbit(wv.y, wv.z, r));
-				o.w = bswap32(__builtin_amdgcn_alignbit(wv.z, wv.w, r));
-				__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
+		lds_barrier(); // B2: this step's image packed; the previous step's offset and predecessor bits
+		if (prev) {
+			const uint32_t fp = f - 1u;
+			const uint32_t P = __builtin_amdgcn_readfirstlane(s_ctl[0]);
+			const uint32_t pred = __builtin_amdgcn_readfirstlane(s_ctl[1]);
+			const uint32_t r = P & 31u, g0 = P >> 5;
+			const uint32_t endbit = P + A_prev;
+			const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
+			const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
+			uint8_t *fdst = a.dst + (uint64_t)fp * a.dst_stride;
+			const __amdgpu_buffer_rsrc_t dst_rsrc =
+				__builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(a.cap & ~3u), 0x00020000);
+			if (data) {
+				// ---- store: funnel shift to the frame bit offset, big-endian ------
+				const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)imgp);
+				const uint32_t nquad = nfull >> 2;
+				for (uint32_t p = tid; p < nquad; p += 256u) {
+					const uint32_t jw = 4u * p;
+					const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + jw);
+					const uint32_t hi = jw ? Ll[jw - 1u] : pred;
+					u32x4 o;
+					o.x = bswap32(__builtin_amdgcn_alignbit(hi, wv.x, r));
+					o.y = bswap32(__builtin_amdgcn_alignbit(wv.x, wv.y, r));
+					o.z = bswap32(__builtin_amdgcn_alignbit(wv.y, wv.z, r));
+					o.w = bswap32(__builtin_amdgcn_alignbit(wv.z, wv.w, r));
+					__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
+				}
+				const uint32_t rr = (tid - nquad) & 255u;
+				if (rr < (nfull & 3u)) {
+					const uint32_t jw = 4u * nquad + rr;
+					const uint32_t hi = jw ? Ll[jw - 1u] : pred;
+					const uint32_t v = __builtin_amdgcn_alignbit(hi, Ll[jw], r);
+					__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
+				}
+			} else if (is_last && lane == 0u) {
+				// ---- frame epilogue (cmp.c:314-334) ---------------------------------
+				if (nfull == J) { // zero-padded final bytes (bitstream_flush)
+					const uint32_t hi = J ? imgp[J - 1u] : pred;
+					const uint32_t v = __builtin_amdgcn_alignbit(hi, imgp[J], r);
+					const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
+					for (uint32_t b = 0; b < nbytes; b++)
+						if (4u * (g0 + J) + b < a.cap)
+							fdst[4u * (g0 + J) + b] = (uint8_t)(v >> (24u - 8u * b));
+				}
+				const uint32_t payload_bytes = (endbit + 7u) >> 3;
+				const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
+				if (a.checksum) {
+					const uint32_t ck = a.checksums[fp];
+					for (uint32_t b = 0; b < 4u; b++)
+						if (payload_bytes + b < a.cap)
+							fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
+				}
+				const uint64_t id =
+					a.ids ? a.ids[fp] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)(acq - 1u) * a.id_astep;
+				uint32_t h[5];
+				if (prim_prev)
+					header_words(h, size, 2u * n, id, hseq_prev, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
+						     ENC_P == ENC_RAW ? 0u : cp.g, ENC_P == ENC_RAW ? 0u : cp.outlier);
+				else
+					header_words(h, size, 2u * n, id, hseq_prev, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S,
+						     a.model_rate, ENC_S == ENC_RAW ? 0u : cs.g, ENC_S == ENC_RAW ? 0u : cs.outlier);
+				const uint32_t hwords = HB_prev == 176u ? 5u : 4u;
+				for (uint32_t wq = 0; wq < hwords; wq++)
+					if (4u * wq + 4u <= a.cap)
+						*reinterpret_cast<uint32_t *>(fdst + 4u * wq) = bswap32(h[wq]);
+				a.status[fp] = size > a.cap ? ERRV(E_DST_TOO_SMALL)
+							    : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
 			}
-			const uint32_t rr = (tid - nquad) & 255u;
-			if (rr < (nfull & 3u)) {
-				const uint32_t jw = 4u * nquad + rr;
-				const uint32_t hi = jw ? Ll[jw - 1u] : pred;
-				const uint32_t v = __builtin_amdgcn_alignbit(hi, Ll[jw], r);
-				__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
-			}
-		} else if (is_last && lane == 0u) {
-			// ---- frame epilogue (cmp.c:314-334) ---------------------------------
-			if (nfull == J) { // zero-padded final bytes (bitstream_flush)
-				const uint32_t hi = J ? img[J - 1u] : pred;
-				const uint32_t v = __builtin_amdgcn_alignbit(hi, img[J], r);
-				const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
-				for (uint32_t b = 0; b < nbytes; b++)
-					if (4u * (g0 + J) + b < a.cap)
-						fdst[4u * (g0 + J) + b] = (uint8_t)(v >> (24u - 8u * b));
-			}
-			const uint32_t payload_bytes = (endbit + 7u) >> 3;
-			const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
-			if (a.checksum) {
-				const uint32_t ck = a.checksums[f];
-				for (uint32_t b = 0; b < 4u; b++)
-					if (payload_bytes + b < a.cap)
-						fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
-			}
-			const uint64_t id = a.ids ? a.ids[f] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)acq * a.id_astep;
-			uint32_t h[5];
-			if (prim)
-				header_words(h, size, 2u * n, id, hseq, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
-					     ENC_P == ENC_RAW ? 0u : cp.g, ENC_P == ENC_RAW ? 0u : cp.outlier);
-			else
-				header_words(h, size, 2u * n, id, hseq, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S, a.model_rate,
-					     ENC_S == ENC_RAW ? 0u : cs.g, ENC_S == ENC_RAW ? 0u : cs.outlier);
-			const uint32_t hwords = HB == 176u ? 5u : 4u;
-			for (uint32_t wq = 0; wq < hwords; wq++)
-				if (4u * wq + 4u <= a.cap)
-					*reinterpret_cast<uint32_t *>(fdst + 4u * wq) = bswap32(h[wq]);
-			a.status[f] = size > a.cap ? ERRV(E_DST_TOO_SMALL)
-						   : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
+			lds_barrier(); // B3: the previous image was read
+			if (wid == 0u)
+				wstamp(a, acq - 1u, 4u);
+			// clear what the previous acquisition used (words 0 .. (A+31)/32 - 1,
+			// and the one after for the flush); it packs acquisition acq + 1
+			const uint32_t nw = (A_prev + 63u) >> 5;
+			for (uint32_t i = tid; i < nw; i += 320u)
+				imgp[i] = 0u;
+			// (visible to the next packing: after the next step's B1)
 		}
-		lds_barrier(); // B3: the image was read
-		if (wid == 0u)
-			wstamp(a, acq, 4u);
-		// clear what this acquisition used (words 0 .. (A+31)/32 - 1, and the
-		// one after for the flush)
-		const uint32_t nw = (A + 63u) >> 5;
-		for (uint32_t i = tid; i < nw; i += 320u)
-			img[i] = 0u;
-		// (the next acquisition's packing comes after its B1)
+		A_prev = A;
+		HB_prev = HB;
+		hseq_prev = hseq;
+		prim_prev = prim;
 	}
 	// the model after the last acquisition, to the work buffer (cmp.c:304-311)
 	if (data) {
@@ -709,6 +743,57 @@ __device__ __forceinline__ void cw_epilogue(uint8_t *fdst, uint32_t cap, uint32_
 		needed[frame] = size;
 }
 
+// The uncompressed fallback of frame f inside the context walk (cmp.c:342-393,
+// after cmp_reset: NONE + UNCOMPRESSED, compress_engine with sequence number
+// 0): the 16-byte header, the samples as big-endian 16-bit words (the low
+// halves for i16-in-i32, sample_reader.h), the checksum, status = raw size;
+// the model takes the samples (a primary pass, cmp.c:305-306).  The samples
+// are read again (the walk keeps only the model).  The attempt's stores are
+// uncounted asm stores: every wave drains them before the barrier, so the raw
+// bytes land after them.
+template <int W, int CH>
+__device__ __forceinline__ void cw_fallback(const WArgs &a, uint32_t f, uint8_t *fdst, uint64_t id, uint32_t flip,
+					 uint32_t (&mdl)[CH][EPT / 2])
+{
+	constexpr uint32_t RW = EPT * W / 16u;
+	const uint32_t tid = threadIdx.x;
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	const u32x4 rsrc = rsrc_words(fdst, a.raw_size & ~3u);
+	const uint8_t *fs = a.src + (uint64_t)f * a.src_stride;
+#pragma unroll
+	for (uint32_t cc = 0; cc < CH; cc++) {
+		const uint32_t first = cc * CW_CHUNK + tid * EPT;
+		const uint4 *p = reinterpret_cast<const uint4 *>(fs + (size_t)first * W);
+		uint4 r[RW];
+#pragma unroll
+		for (uint32_t q = 0; q < RW; q++)
+			r[q] = p[q];
+		uint32_t w[EPT / 2];
+		cw_pairs<W>(r, flip, w);
+#pragma unroll
+		for (uint32_t q = 0; q < EPT / 2; q++) {
+			mdl[cc][q] = w[q];
+			const uint32_t x = w[q] ^ flip; // the samples
+			w[q] = ((x & 0x00FF00FFu) << 8) | ((x >> 8) & 0x00FF00FFu);
+		}
+#pragma unroll
+		for (uint32_t q = 0; q < EPT / 8; q++)
+			store_b128_nc((u32x4){w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]}, 16u + 2u * first + 16u * q,
+				      rsrc);
+	}
+	if (tid == 0u) {
+		uint32_t h[5];
+		header_words(h, a.raw_size, 2u * a.n, id, 0u, PRE_NONE, a.checksum ? 1u : 0u, ENC_RAW, 0u, 0u, 0u);
+#pragma unroll
+		for (uint32_t wq = 0; wq < 4u; wq++)
+			store_b32_nc(bswap32(h[wq]), 4u * wq, rsrc);
+		if (a.checksum)
+			store_b32_nc(bswap32(a.checksums[f]), 16u + 2u * a.n, rsrc);
+		a.status[f] = a.raw_size;
+	}
+}
+
 template <int W, int PRE_P, int ENC_P, bool RICE_P, int ENC_S, bool RICE_S, int CH>
 __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 {
@@ -845,9 +930,18 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 			else
 				cw_chunk<ENC_S, RICE_S>(st, img, imgo, s_wsum, cc & 1u, T, mp, oq, cs, fast_s, tab_s, dst_rsrc);
 		}
-		if (tid == 0u) {
-			const uint32_t size = ((st.P + 7u) >> 3) + (a.checksum ? 4u : 0u);
-			const uint64_t id = a.ids ? a.ids[f] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)acq * a.id_astep;
+		const uint32_t size = ((st.P + 7u) >> 3) + (a.checksum ? 4u : 0u);
+		const uint64_t id = a.ids ? a.ids[f] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)acq * a.id_astep;
+		// the uncompressed fallback (cmp.c:342-393): the attempt ran with the
+		// raw frame size as its capacity (a.cap); a frame that does not fit is
+		// reset and written raw (block-uniform: st.P is)
+		const bool fbk = a.fb && size > a.raw_size;
+		if (a.draws && tid == 0u) // identifier draws: one per reset (cmp.c:228-231, 371-392)
+			a.draws[f] = (uint8_t)(prim ? (fbk ? 3u : 1u) : (fbk ? 2u : 0u));
+		if (fbk) {
+			cw_fallback<W, CH>(a, f, fdst, id, flip, mdl);
+			sq = 1u; // the fallback frame has sequence number 0, the next 1
+		} else if (tid == 0u) {
 			uint32_t h[5];
 			if (prim)
 				header_words(h, size, 2u * n, id, hseq, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
@@ -859,6 +953,8 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 				    a.status, nullptr, f, size);
 		}
 	}
+	if (a.seq_out && tid == 0u)
+		a.seq_out[c] = (uint8_t)sq;
 	// the model after the last acquisition, to the work buffer (cmp.c:304-311)
 #pragma unroll
 	for (uint32_t cc = 0; cc < CH; cc++) {
@@ -942,7 +1038,7 @@ bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint
 bool walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
 		 bool rice_s, hipStream_t s)
 {
-	const size_t lds = (size_t)(k.img_words + 4u) * 4u;
+	const size_t lds = (size_t)(2u * k.img_words + 8u) * 4u; // two images (walk_kernel)
 	if (sample_bytes == 2)
 		return pre_p == PRE_DIFF ? walk_launch_p<2, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
 					 : walk_launch_p<2, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);

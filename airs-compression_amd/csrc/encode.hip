@@ -969,6 +969,7 @@ struct airs_dev_engine {
 	size_t gran_cap; // segments
 	uint32_t *ticket;
 	uint32_t ticket_base;
+	uint32_t walk_ticket_base; // ticket[AIRS_WALK_TICKET] before the next segment walk
 	uint32_t epoch;
 	void *scratch[AIRS_NSLOT];
 	size_t scratch_cap[AIRS_NSLOT];
@@ -1447,6 +1448,26 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 
 // ---- MODEL streams in one launch (enc_walk.hip) ----------------------------
 
+// contexts from which a batch of walk_ctx_samples()-sample frames takes the
+// context walk (one workgroup per context) instead of the segment walk
+#ifndef AIRS_WALK_CTX_MIN
+#define AIRS_WALK_CTX_MIN 128u
+#endif
+
+// words of ONE of the context walk's two images (16384 samples of the
+// longer-coded pass), or 0 when the batch does not take the context walk:
+// frames of its size, enough contexts to fill the CUs, two images in the LDS
+static uint32_t ctx_walk_words(const struct airs_walk *w)
+{
+	const uint32_t mbp = code_max_bits(w->enc_p, w->g_p, w->outl_p);
+	const uint32_t mbs = code_max_bits(w->enc_s, w->g_s, w->outl_s);
+	const uint32_t mb = mbp > mbs ? mbp : mbs;
+	const uint32_t cw = ((walk_ctx_samples() / 4u * mb / 32u + 8u) + 3u) & ~3u;
+	if (w->n == walk_ctx_samples() && w->num_ctx >= AIRS_WALK_CTX_MIN && (2u * cw + 4u) * 4u <= 150u * 1024u)
+		return cw;
+	return 0u;
+}
+
 extern "C" int airs_dev_walk_supported(const struct airs_walk *w)
 {
 	if (!w || !w->n || w->n % AIRS_SEG || !w->num_ctx || !w->fpc || (w->sample_bytes != 2 && w->sample_bytes != 4))
@@ -1458,15 +1479,13 @@ extern "C" int airs_dev_walk_supported(const struct airs_walk *w)
 		return 0;
 	if (!w->model_ptrs && (((uintptr_t)w->model & 15u) || (w->model_stride & 15u)))
 		return 0;
+	if (w->fb && (!w->draws || !w->seq_out || w->cap != w->raw_size || w->raw_size < 16u + 2u * w->n ||
+		      !ctx_walk_words(w)))
+		return 0;
 	const uint64_t segs = (uint64_t)w->num_ctx * (w->n / AIRS_SEG);
 	return segs <= 0x7FFFFFFFull && segs * w->fpc <= 0x7FFFFFFFull;
 }
 
-// contexts from which a batch of walk_ctx_samples()-sample frames takes the
-// context walk (one workgroup per context) instead of the segment walk
-#ifndef AIRS_WALK_CTX_MIN
-#define AIRS_WALK_CTX_MIN 128u
-#endif
 
 extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_walk *w)
 {
@@ -1510,6 +1529,10 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 	k.outl_s = w->outl_s;
 	k.model_rate = w->model_rate;
 	k.is_unsigned = w->is_unsigned;
+	k.fb = w->fb ? 1u : 0u;
+	k.raw_size = w->raw_size;
+	k.draws = w->draws;
+	k.seq_out = w->seq_out;
 	// one image for the longer-coded of the two passes (plus a flush word)
 	const uint32_t iw_p = image_words(w->enc_p, w->g_p), iw_s = image_words(w->enc_s, w->g_s);
 	k.img_words = (iw_p > iw_s ? iw_p : iw_s) + 4u;
@@ -1517,11 +1540,8 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 	// one context per workgroup when the frames have its size, there are
 	// enough contexts to fill the CUs, and two images fit the LDS
 	{
-		const uint32_t mbp = code_max_bits(w->enc_p, w->g_p, w->outl_p);
-		const uint32_t mbs = code_max_bits(w->enc_s, w->g_s, w->outl_s);
-		const uint32_t mb = mbp > mbs ? mbp : mbs;
-		const uint32_t cw = ((walk_ctx_samples() / 4u * mb / 32u + 8u) + 3u) & ~3u;
-		if (w->n == walk_ctx_samples() && w->num_ctx >= AIRS_WALK_CTX_MIN && (2u * cw + 4u) * 4u <= 150u * 1024u) {
+		const uint32_t cw = ctx_walk_words(w);
+		if (cw) {
 			WArgs kc = k;
 			kc.img_words = cw;
 			if (!walk_ctx_encode(kc, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream))
@@ -1530,6 +1550,9 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 			return 0;
 		}
 	}
+	// the fallback runs in the context walk only
+	if (w->fb)
+		return ERRV(E_PARAMS_INVALID);
 #if AIRS_ABLATE
 	k.dbg = g_dbg;
 	if (g_dbg & 65536) {
@@ -1544,9 +1567,12 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 		k.dbgts = e->dbgts;
 	}
 #endif
+	// images: the longer-coded pass's 4096 samples, plus the flush word
+	k.ticket_base = e->walk_ticket_base;
 	if (!walk_encode(k, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream))
 		return ERRV(E_PARAMS_INVALID);
 	HIPCHECK(hipGetLastError());
+	e->walk_ticket_base += (uint32_t)(w->num_ctx * spf);
 	return 0;
 }
 

@@ -88,6 +88,12 @@ WORKLOADS = {
                              secondary_encoder_type=MULTI, secondary_encoder_param=8,
                              secondary_encoder_outlier=107, model_rate=11)),
 }
+# configs[4] as ONE GPU of an 8-GPU node holds it (streams s mod 8, rank 0's
+# shard: 32 streams): the per-GPU work of the 8-GPU strong-scaling run of
+# configs[4]
+WORKLOADS["cfg5s8"] = dict(WORKLOADS["cfg5"], nctx=32, shard=(0, 8),
+                           desc="configs[4], rank 0's shard at N = 8: streams 0, 8, ..., 248 (32 streams x 16 "
+                                "acquisitions x 64 Ki i16-in-i32), parameters of cfg5")
 # configs[4] with the uncompressed fallback enabled: every frame may fall back,
 # so the batch runs the context state machine on the device (the frames are
 # those of cfg5: this data always compresses)
@@ -130,6 +136,8 @@ def measured_traffic(wname):
 def frame_ids(wl, rank, world):
     """global frame numbers of this rank's frames, in local order (shard.py layouts)"""
     nf, fpc = wl["nctx"] * wl["fpc"], wl["fpc"]
+    if wl.get("shard"):  # one fixed rank's shard of a larger node (cfg5s8)
+        rank, world = wl["shard"]
     if wl["layout"] == "roundrobin":
         return [rank + world * j for j in range(nf)]
     if wl["layout"] == "streams":  # stream s on rank s mod N (its model stays on one GPU)
@@ -442,7 +450,9 @@ def main():
     with open(os.path.join(ROOT, "tests", "golden", gfile)) as f:
         gold = json.load(f)["cases" if wl.get("stream") else "configs"][wl["golden"]]
     key = f"shard_digests_n{world}" if wl["layout"] == "roundrobin" else None
-    if key and key in gold:
+    if wl.get("shard"):
+        want = gold[f"shard_digests_n{wl['shard'][1]}"][wl["shard"][0]] if world == 1 else None
+    elif key and key in gold:
         want = gold[key][rank]
     elif wl["layout"] in ("block", "streams") and world == 1:
         want = gold["sha256"] if wl.get("stream") else gold["digest"]
@@ -520,6 +530,9 @@ def main():
         "cfg4": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL>: one launch per step",
         "cfg5": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> (enc_walk.hip): ONE launch per step, one "
                 "1024-thread workgroup per stream walks its 16 acquisitions, the model in registers",
+        "cfg5s8": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice> (enc_walk.hip, the segment walk): ONE launch per "
+                  "step, a 320-thread workgroup per (stream, 4096-sample segment) walks the 16 acquisitions, each "
+                  "acquisition's look-back resolved one step later",
         "cfg5fb": "per acquisition: fb_step_kernel + fb_copy_kernel + encode_kernel<4,DIFF,ZERO,Rice,STORE> + "
                   "encode_kernel<4,MODEL,MULTI,Rice,UPDATE> (frame-list holes)",
     }

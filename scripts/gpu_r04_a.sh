@@ -7,3 +7,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; tail -5 $O/pytest_gpu.log
 [ $rc -eq 0 ] || [ -n "$SKIP_TESTS_OK" ] || exit $rc
 bash scripts/gpu_envab.sh $TAG
+for w in ${BENCH_WLS:-}; do
+  timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline --steps 10 --warmup 3 > $O/bench_$w.json 2> $O/bench_$w.err || { tail -5 $O/bench_$w.err; exit 1; }
+  cut -c1-400 $O/bench_$w.json
+done

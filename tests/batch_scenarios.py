@@ -49,9 +49,23 @@ def _per_ctx(params, nctx):
     return list(params) if isinstance(params, (list, tuple)) else [params] * nctx
 
 
-def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000, primary_g=None):
+def _calls(fpc, splits):
+    """(first acquisition, acquisitions) of each cmp_gpu_compress call"""
+    splits = list(splits) if splits else [fpc]
+    assert sum(splits) == fpc
+    out, a0 = [], 0
+    for k in splits:
+        out.append((a0, k))
+        a0 += k
+    return out
+
+
+def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000, primary_g=None, splits=None):
     """primary_g: optional src -> g, set as the context's primary encoder
-    parameter before each call (the CMP_GPU_AUTO_RICE rule)"""
+    parameter before each call (the CMP_GPU_AUTO_RICE rule).  splits: the
+    acquisitions per cmp_gpu_compress call when the GPU side makes several
+    calls on the same contexts (the loop order is then call by call, c-major
+    inside a call); frames are returned in (context, acquisition) order."""
     sb = 4 if kind == "i16_in_i32" else 2
     pcs = _per_ctx(params, nctx)
     lib.set_timestamp_func(_ts_counter(ts_start))
@@ -63,14 +77,15 @@ def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=500
             w = _work_size(lib, api, pcs[c], n * sb)
             r = lib.initialise(ctxs[c], pcs[c], wbs_bufs[c] if w else None, w)
             assert not api.is_error(r), api.error_name(r)
-        frames = []
-        for c in range(nctx):
-            for a in range(fpc):
-                dst = api.aligned_empty(cap + 64, fill=0xAB)
-                if primary_g is not None:
-                    ctxs[c].params.primary_encoder_param = primary_g(srcs[c * fpc + a])
-                r = lib.compress(kind, ctxs[c], dst, cap, srcs[c * fpc + a])
-                frames.append((r, bytes(dst[:r]) if not api.is_error(r) else None))
+        frames = [None] * (nctx * fpc)
+        for a0, k in _calls(fpc, splits):
+            for c in range(nctx):
+                for a in range(a0, a0 + k):
+                    dst = api.aligned_empty(cap + 64, fill=0xAB)
+                    if primary_g is not None:
+                        ctxs[c].params.primary_encoder_param = primary_g(srcs[c * fpc + a])
+                    r = lib.compress(kind, ctxs[c], dst, cap, srcs[c * fpc + a])
+                    frames[c * fpc + a] = (r, bytes(dst[:r]) if not api.is_error(r) else None)
         state = [(x.identifier, x.sequence_number, x.model_size, bytes(w[:wbs]))
                  for x, w in zip(ctxs, wbs_bufs)]
         return tuple(frames), tuple(state)
@@ -78,13 +93,16 @@ def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=500
         lib.set_timestamp_func(None)
 
 
-def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000, flags=0):
+def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000, flags=0, splits=None):
     import torch
     sb = 4 if kind == "i16_in_i32" else 2
     pcs = _per_ctx(params, nctx)
     nf = nctx * fpc
     stride = n * sb
-    host_src = np.concatenate([np.ascontiguousarray(s).view(np.uint8) for s in srcs])
+    calls = _calls(fpc, splits)
+    # batch order: call by call, c-major inside a call
+    order = [c * fpc + a for a0, k in calls for c in range(nctx) for a in range(a0, a0 + k)]
+    host_src = np.concatenate([np.ascontiguousarray(srcs[f]).view(np.uint8) for f in order])
     src = torch.from_numpy(host_src).cuda()
     dstride = (cap + 64 + 7) // 8 * 8
     dst = torch.full((nf * dstride,), 0xAB, dtype=torch.uint8, device="cuda")
@@ -100,17 +118,20 @@ def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start
             r = lib.initialise(ctxs[c], pcs[c], (work.data_ptr() + c * wstride) if w else None, w)
             assert not api.is_error(r), api.error_name(r)
         torch.cuda.synchronize()
-        r = eng.compress(ctxs, fpc, kind, src.data_ptr(), stride, stride, dst.data_ptr(), dstride, cap,
-                         sizes.data_ptr(), flags)
-        assert r == 0, api.error_name(r)
+        off = 0
+        for a0, k in calls:
+            r = eng.compress(ctxs, k, kind, src.data_ptr() + off * stride, stride, stride,
+                             dst.data_ptr() + off * dstride, dstride, cap, sizes.data_ptr() + 4 * off, flags)
+            assert r == 0, api.error_name(r)
+            off += nctx * k
         assert eng.synchronize() == 0
         sz = sizes.cpu().numpy().astype(np.uint32)
         host = dst.cpu().numpy()
         wk = work.cpu().numpy()
-        frames = []
-        for f in range(nf):
-            s = int(sz[f])
-            frames.append((s, bytes(host[f * dstride:f * dstride + s]) if not api.is_error(s) else None))
+        frames = [None] * nf
+        for j, f in enumerate(order):
+            s = int(sz[j])
+            frames[f] = (s, bytes(host[j * dstride:j * dstride + s]) if not api.is_error(s) else None)
         state = [(ctxs[c].identifier, ctxs[c].sequence_number, ctxs[c].model_size,
                   bytes(wk[c * wstride:c * wstride + wbs])) for c in range(nctx)]
         return tuple(frames), tuple(state)

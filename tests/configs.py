@@ -149,6 +149,13 @@ def reference_digest(name, lib_path):
             d[f"shard_digests_n{nw}"] = [frame_digest(frames[r::nw][:1024])["digest"] for r in range(nw)]
             # what rank 0 holds after gathering N shards: frames 0 .. 1024*N-1 in f order
             d[f"gather_digest_n{nw}"] = frame_digest(frames[:1024 * nw])["digest"]
+    if name == "cfg5_model":
+        # streams sharded s mod N (bench.py cfg5 shard workloads): rank r of N
+        # holds streams r, r + N, ..., each stream's 16 frames in order
+        fpc, ns = CONFIGS[name]["fpc"], CONFIGS[name]["nctx"]
+        for nw in (2, 4, 8):
+            d[f"shard_digests_n{nw}"] = [frame_digest([frames[s * fpc + a] for s in range(r, ns, nw)
+                                                       for a in range(fpc)])["digest"] for r in range(nw)]
     if gs is not None:
         d["rice_g_digest"] = hashlib.sha256(np.array(gs, dtype=np.uint32).tobytes()).hexdigest()
     return d

@@ -243,10 +243,17 @@ def gen_random(ref):
     print("random sequences:", len(seqs), "ok frames:", sum(s["ok_frames"] for s in seqs))
 
 
-def gen_configs():
+def gen_configs(only=None):
+    """only: config names to regenerate (the others are kept from the file)"""
     import configs as cfgmod
     res = {}
+    path = os.path.join(HERE, "configs.json")
+    if only and os.path.exists(path):
+        with open(path) as f:
+            res = json.load(f)["configs"]
     for name in cfgmod.CONFIGS:
+        if only and name not in only:
+            continue
         res[name] = cfgmod.reference_digest(name, REF_PATH)
         print(name, res[name])
     with open(os.path.join(HERE, "configs.json"), "w") as f:
@@ -256,7 +263,7 @@ def gen_configs():
 
 
 def main():
-    """usage: gen_golden.py [kats] [random] [configs]   (default: all three)"""
+    """usage: gen_golden.py [kats] [random] [configs | configs:NAME,...]   (default: all three)"""
     stages = [a for a in sys.argv[1:] if not a.startswith("-")] or ["kats", "random", "configs"]
     ref = api.CmpLib(REF_PATH)
     orc = api.CmpLib(ORC_PATH)
@@ -266,6 +273,9 @@ def main():
         gen_random(ref)
     if "configs" in stages:
         gen_configs()
+    for st in stages:  # configs:NAME[,NAME]: regenerate those configs only
+        if st.startswith("configs:"):
+            gen_configs(st.split(":", 1)[1].split(","))
 
 
 if __name__ == "__main__":

@@ -125,6 +125,8 @@ int airs_dev_walk_supported(const struct airs_walk *w)
 		return 0;
 	if (((uintptr_t)w->src & 15u) || (w->src_stride & 15u))
 		return 0;
+	if (w->fb && (!w->draws || !w->seq_out || w->cap != w->raw_size))
+		return 0;
 	return w->model_ptrs || !(((uintptr_t)w->model & 15u) || (w->model_stride & 15u));
 }
 
@@ -159,7 +161,11 @@ uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_walk *w)
 			memset(dst, 0, 16);
 			dst[size - 1u] = 0x5A;
 			w->status[f] = size;
+			if (w->fb) /* the walk's fallback: identifier draws of the frame */
+				w->draws[f] = (uint8_t)(h >> 40) & 3u;
 		}
+		if (w->fb)
+			w->seq_out[c] = (uint8_t)(1u + c % 3u);
 	}
 	return 0;
 }

@@ -133,6 +133,53 @@ def test_batch_model_fallback_cfg5_shape(prod, eng, orc, exact_mode, kind):
     assert got == want
 
 
+@pytest.mark.parametrize("kind", ["i16_in_i32", "u16"])
+@pytest.mark.parametrize("flags", [0, api.GPU_STEPWISE], ids=["walk", "stepwise"])
+def test_batch_walk_fallback_cfg5_shape(prod, eng, orc, kind, flags):
+    """BASELINE config 5's shape with the uncompressed fallback (cfg5fb):
+    128 contexts of 64 Ki-sample frames, so the batch takes the context walk
+    with the fallback resolved on the chip (flags 0: one launch, the frame that
+    does not fit its raw size is written raw, the model takes its samples, the
+    context continues at sequence number 1; then the host draws the
+    identifiers from the reported draw counts), against the per-acquisition
+    device state machine (CMP_GPU_STEPWISE) and the oracle's call loop.  Noise
+    frames at scattered steps fall back as primary and as secondary passes;
+    two calls on the same contexts, so the second starts from contexts in
+    different states.  Frames with identifiers unmasked, sizes, context
+    states and work buffers."""
+    import numpy as np
+    P = api.CmpParams
+    params = P(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16,
+               secondary_iterations=15, secondary_preprocessing=3, secondary_encoder_type=2,
+               secondary_encoder_param=8, secondary_encoder_outlier=107, model_rate=11,
+               checksum_enabled=1, uncompressed_fallback_enabled=1)
+    rng = np.random.default_rng(66 + len(kind))
+    n, nctx, fpc = 65536, 128, 5
+    srcs = []
+    for c in range(nctx):
+        base = np.cumsum(rng.integers(-3, 4, n))
+        for a in range(fpc):
+            if rng.random() < 0.12:
+                v = rng.integers(-32768, 32768, n)  # noise: the frame falls back
+            else:
+                v = base + rng.integers(-4, 5, n)
+            v = v.astype(np.int64)
+            if kind == "u16":
+                srcs.append((v & 0xFFFF).astype(np.uint16))
+            else:
+                srcs.append(((v & 0xFFFF) | (rng.integers(-5, 5, n) << 16)).astype(np.int32))
+    cap = 26 + 6 * n
+    splits = [2, 3]
+    want = bs.run_batch_host(orc, api, params, kind, n, nctx, fpc, cap, srcs, splits=splits)
+    heads = [api.parse_header(b) for r, b in want[0] if b is not None]
+    nfb = sum(1 for h in heads if h["encoder_type"] == 0)
+    assert nfb > 30, nfb
+    got = bs.run_batch_gpu(prod, eng, api, params, kind, n, nctx, fpc, cap, srcs, flags=flags, splits=splits)
+    assert got[1] == want[1], "context states or work buffers differ"
+    bad = [f for f in range(nctx * fpc) if got[0][f] != want[0][f]]
+    assert not bad, f"frames {bad[:8]} differ"
+
+
 def test_batch_mixed_fallback_model_contexts(prod, eng, orc):
     """contexts with and without the uncompressed fallback
     in one batch (different parameters: the host-stepped path), with

@@ -234,16 +234,17 @@ CTX_CASES = [  # (kind, pre_p, enc_p, g_p, o_p, enc_s, g_s, o_s, iters, rate, ch
 ]
 
 
-@pytest.mark.parametrize("case", range(len(CTX_CASES)))
-def test_walk_ctx_vs_call_loop(prod, eng, orc, case):
+@pytest.mark.parametrize("case,nctx", [(c, 128) for c in range(len(CTX_CASES))] + [(0, 32), (4, 32)])
+def test_walk_ctx_vs_call_loop(prod, eng, orc, case, nctx):
     """Batches of >= 128 contexts of 64 Ki-sample frames take the context walk
-    (one workgroup per context, walk_ctx_kernel): frames, sizes, context
-    states and work buffers equal the call loop; two calls in a row, so the
-    second starts mid-sequence with the model read back from the work
-    buffers."""
+    (one workgroup per context, walk_ctx_kernel); 32 contexts (configs[4]'s
+    per-GPU share at N = 8) take the segment walk (walk_kernel, each
+    acquisition's look-back one step late).  Frames, sizes, context states and
+    work buffers equal the call loop; two calls in a row, so the second starts
+    mid-sequence with the model read back from the work buffers."""
     kind, pre, ep, gp, op, es, gs, osx, iters, rate, ck = CTX_CASES[case]
-    rng = np.random.default_rng(500 + case)
-    n, nctx = 65536, 128
+    rng = np.random.default_rng(500 + case + nctx)
+    n = 65536
     p = P(primary_preprocessing=pre, primary_encoder_type=ep, primary_encoder_param=gp, primary_encoder_outlier=op,
           secondary_iterations=iters, secondary_preprocessing=3, secondary_encoder_type=es,
           secondary_encoder_param=gs, secondary_encoder_outlier=osx, model_rate=rate, checksum_enabled=ck)
@@ -312,5 +313,27 @@ def test_whole_unit_frames_vs_call_loop(prod, eng, orc, case):
     got = run_gpu(prod, eng, [p], kind, n, 1, calls, cap)
     (fw, sw), (fg, sg) = want[0], got[0]
     bad = [f for f in range(nfr) if fw[f] != fg[f]]
+    assert not bad, f"frames {bad[:8]} differ"
+    assert sw == sg
+
+
+def test_segment_walk_more_workgroups_than_resident(prod, eng, orc):
+    """a segment walk whose grid exceeds what the GPU holds at once
+    (1100 contexts x one 4096-sample segment, 320-thread workgroups with two
+    images each, fewer than 1100 resident) and a long walk (12 acquisitions):
+    the workgroups take logical indices from a ticket, so a look-back only
+    waits on a running workgroup; no give-up, frames and state equal the call
+    loop."""
+    rng = np.random.default_rng(31)
+    kind, n, nctx, fpc = "u16", 4096, 1100, 12
+    p = P(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16, secondary_iterations=15,
+          secondary_preprocessing=3, secondary_encoder_type=2, secondary_encoder_param=8,
+          secondary_encoder_outlier=107, model_rate=11, checksum_enabled=1)
+    calls = [(fpc, make_frames(kind, n, nctx * fpc, rng))]
+    cap = 26 + 6 * n
+    want = run_host(orc, [p] * nctx, kind, n, nctx, calls, cap)
+    got = run_gpu(prod, eng, [p] * nctx, kind, n, nctx, calls, cap)
+    (fw, sw), (fg, sg) = want[0], got[0]
+    bad = [f for f in range(len(fw)) if fw[f] != fg[f]]
     assert not bad, f"frames {bad[:8]} differ"
     assert sw == sg
