@@ -52,12 +52,22 @@ namespace airs {
 #ifndef AIRS_ARENA_DEFAULT         // eligible launches take the arena kernel
 #define AIRS_ARENA_DEFAULT 1
 #endif
+#ifndef AIRS_ARENA_CTL_DEFAULT     // the control-wave form (arena_kernel CTL)
+#define AIRS_ARENA_CTL_DEFAULT 0
+#endif
 #ifndef AIRS_ARENA_WORDS_DEFAULT   // arena words: 6400 = 12.5 bits per sample, ~25 KiB of LDS
 #define AIRS_ARENA_WORDS_DEFAULT 6400u
 #endif
 
-template <int PRE, bool STREAM>
-__global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_WPE, 8))) void arena_kernel(KArgs a)
+// CTL: a fifth wave (the control wave) owns the look-back: it issues the
+// scalar granule loads before the packing starts (its barrier instruction
+// inside the same asm statement, so that nothing waits for them) and has the
+// frame offset in LDS by the barrier that ends the packing; the four data
+// waves never wait for the round trip.  Without CTL, wave 0 evaluates the
+// look-back after the packing.
+template <int PRE, bool STREAM, bool CTL>
+__global__ __launch_bounds__(EWG + (CTL ? 64 : 0)) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_WPE, 8))) void
+arena_kernel(KArgs a)
 {
 	static_assert(EPT == 16u, "lane t owns samples [16t, 16t+16) of a chunk");
 	constexpr uint32_t HDR_BITS = STREAM ? 0u : 176u; // 22-byte header (GOLOMB_ZERO)
@@ -74,6 +84,9 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_
 
 	const uint32_t tid = threadIdx.x, lane = tid & 63u;
 	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const bool ctl = CTL && wid == EWG / 64; // the control wave
+	const bool data = !ctl;
+	const uint32_t lbw = CTL ? EWG / 64 : 0u; // the wave that runs the look-back
 	// frame-interleaved dispatch (encode_kernel): consecutive blocks take the
 	// same segment index of consecutive frames
 	const uint32_t seg = blockIdx.x;
@@ -93,7 +106,7 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_
 	uint4 raw[ACH][2];
 	uint32_t prevld[ACH];
 #pragma unroll
-	for (uint32_t c = 0; c < ACH; c++) {
+	for (uint32_t c = 0; c < ACH && data; c++) {
 		const uint32_t first = sif * ASEGN + c * AIRS_SEG + tid * EPT;
 		const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)first * 2u);
 		raw[c][0] = p[0];
@@ -114,6 +127,9 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_
 	uint32_t T[ACH];           // this lane's bits in chunk c
 #pragma unroll
 	for (uint32_t c = 0; c < ACH; c++) {
+		T[c] = 0u;
+		if (!data)
+			continue;
 		uint32_t w[EPT / 2];
 #pragma unroll
 		for (uint32_t q = 0; q < 2u; q++) {
@@ -150,7 +166,7 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_
 #pragma unroll
 	for (uint32_t c = 0; c < ACH; c++) {
 		inc[c] = wave_incl_scan(T[c]);
-		if (lane == 63u)
+		if (lane == 63u && data)
 			s_wsum[c][wid] = inc[c];
 	}
 	__syncthreads(); // B1: wave totals and the code table visible
@@ -171,7 +187,7 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_
 	}
 	base[ACH] = A;
 	const uint32_t first_seg = gseg - sif;
-	if (wid == 0 && lane == 0) {
+	if (wid == lbw && lane == 0) {
 		const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
 		gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
 	}
@@ -253,6 +269,120 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_
 		}
 	};
 
+	// ---- the look-back (wave lbw) ---------------------------------------
+	// First round: the 64 newest granules through vector loads for segments
+	// with fewer than SLB_N predecessors in their frame; else the SLB_N newest
+	// (and the predecessor's tail) through scalar loads, which do not queue
+	// behind the CU's sample loads.  slb_load issues them and
+	// waits in ONE asm statement (lgkmcnt also counts LDS operations, and no
+	// register of an outstanding load may be visible to the compiler); with
+	// CTL the statement also holds the control wave's barrier B2.
+	typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+	auto sptr = [](const uint64_t *p) {
+		const uint64_t v = (uint64_t)(uintptr_t)p;
+		const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)v);
+		const uint32_t h = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+		return (const uint64_t *)(uintptr_t)(((uint64_t)h << 32) | l);
+	};
+	auto slb_load = [&](uint64_t &gv, uint64_t &tv0, bool with_barrier) {
+		const uint64_t *gp = sptr(&a.agg[gseg - SLB_N]);
+		const uint64_t *tp = sptr(&a.tail[gseg - 1u]);
+		u32x16 q[2];
+		uint64_t tq;
+		if (with_barrier)
+			asm volatile("s_load_dwordx16 %0, %3, 0x0 glc\n\t"
+				     "s_load_dwordx16 %1, %3, 0x40 glc\n\t"
+				     "s_load_dwordx2 %2, %4, 0x0 glc\n\t"
+				     "s_barrier\n\t"
+				     "s_waitcnt lgkmcnt(0)"
+				     : "=&s"(q[0]), "=&s"(q[1]), "=&s"(tq)
+				     : "s"(gp), "s"(tp)
+				     : "memory");
+		else
+			asm volatile("s_load_dwordx16 %0, %3, 0x0 glc\n\t"
+				     "s_load_dwordx16 %1, %3, 0x40 glc\n\t"
+				     "s_load_dwordx2 %2, %4, 0x0 glc\n\t"
+				     "s_waitcnt lgkmcnt(0)"
+				     : "=&s"(q[0]), "=&s"(q[1]), "=&s"(tq)
+				     : "s"(gp), "s"(tp)
+				     : "memory");
+		// granule gseg - SLB_N + i -> lane SLB_N - 1 - i; lanes >= SLB_N read as
+		// unpublished (tag 0).  (v_writelane: no per-lane compares, which the
+		// compiler hoisted and spilled)
+		uint32_t vl = 0u, vh = 0u;
+#pragma unroll
+		for (uint32_t i = 0; i < SLB_N; i++) {
+			asm("v_writelane_b32 %0, %1, %2" : "+v"(vl) : "s"(q[i >> 3][2u * (i & 7u)]), "n"(SLB_N - 1u - i));
+			asm("v_writelane_b32 %0, %1, %2" : "+v"(vh) : "s"(q[i >> 3][2u * (i & 7u) + 1u]), "n"(SLB_N - 1u - i));
+		}
+		gv = ((uint64_t)vh << 32) | vl;
+		tv0 = tq;
+	};
+	auto vec_load = [&](uint64_t &gv, uint64_t &tv0) {
+		const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane;
+		gv = gran_load(&a.agg[idx >= (int64_t)first_seg ? idx : (int64_t)first_seg]);
+		tv0 = gran_load(&a.tail[gseg - 1u]);
+	};
+	// rounds until an inclusive prefix: the frame offset P, published as this
+	// segment's inclusive prefix; the predecessor's tail; both to LDS
+	auto evaluate = [&](uint64_t gv, uint64_t tv0) {
+		uint32_t Pw = HDR_BITS, prd = 0u;
+		if (is_first) {
+			// header bytes 20-21 (low half of the outlier field) share the
+			// first payload dword of the 22-byte header
+			prd = STREAM ? 0u : (cd.outlier & 0xFFFFu);
+		} else {
+			uint32_t sum = 0u, spins = 0u;
+			int64_t j = (int64_t)gseg - 1;
+			for (;;) {
+				const int64_t idx = j - (int64_t)lane;
+				const bool inr = idx >= (int64_t)first_seg;
+				const uint32_t tag = (uint32_t)(gv >> 32);
+				const bool valid = inr && (tag >> 1) == a.epoch;
+				const bool incl = valid && (tag & 1u);
+				const uint64_t incl_m = __ballot(incl);
+				const uint64_t bad_m = __ballot(inr && !valid);
+				const uint32_t fi = incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
+				const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
+				if (bad_m & need) {
+					// a needed predecessor has not published: re-poll this window
+					if (++spins > AIRS_SPIN_LIMIT) {
+						if (lane == 0)
+							atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+						break;
+					}
+					__builtin_amdgcn_s_sleep(1);
+				} else {
+					sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv : 0u);
+					if (incl_m)
+						break;
+					j -= 64;
+				}
+				const int64_t id2 = j - (int64_t)lane;
+				gv = id2 >= (int64_t)first_seg ? gran_load(&a.agg[id2]) : 0ull;
+			}
+			Pw = sum;
+			if (lane == 0)
+				gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (Pw + A));
+			if (lane == 0) {
+				uint64_t tv = tv0;
+				for (uint32_t sp = 0; (uint32_t)(tv >> 32) != a.epoch; sp++) {
+					if (sp > AIRS_SPIN_LIMIT) {
+						atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+						break;
+					}
+					__builtin_amdgcn_s_sleep(1);
+					tv = gran_load(&a.tail[gseg - 1u]);
+				}
+				prd = (uint32_t)tv;
+			}
+		}
+		if (lane == 0) {
+			s_misc[1] = Pw;
+			s_misc[2] = prd;
+		}
+	};
+
 	// ---- phase 2: passes of whole chunks -> the arena -> HBM ----------------
 	// one pass of all four chunks when the segment fits the arena, else one
 	// pass per chunk (uniform: A is block-uniform)
@@ -270,25 +400,31 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_
 		// read the arena before the barrier that ended its look-back / pass)
 		if (ps)
 			__syncthreads();
-		{
+		if (data) {
 			uint4 *Z = reinterpret_cast<uint4 *>(AR);
 			const uint32_t nz4 = (((pbits + 31u) >> 5) + 4u) >> 2;
 			for (uint32_t i = tid; i < nz4; i += EWG)
 				Z[i] = make_uint4(0u, 0u, 0u, 0u);
 		}
-		__syncthreads(); // B2: arena zeroed
 		uint64_t gv = 0, tv0 = 0;
-		const bool vec_lb = ps == 0 && !is_first && sif < SLB_N;
-		if (vec_lb && wid == 0) {
-			// first look-back round, vector loads (few predecessors): issued
-			// here, evaluated after the packing
-			const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane;
-			gv = gran_load(&a.agg[idx >= (int64_t)first_seg ? idx : (int64_t)first_seg]);
-			tv0 = gran_load(&a.tail[gseg - 1u]);
+		const bool lb = ps == 0 && !is_first; // this pass runs the look-back
+		if (CTL && ctl) {
+			// B2 for the control wave, with the first round's loads in flight
+			if (lb && sif >= SLB_N) {
+				slb_load(gv, tv0, true);
+			} else {
+				if (lb)
+					vec_load(gv, tv0);
+				asm volatile("s_barrier" ::: "memory");
+			}
+		} else {
+			__syncthreads(); // B2: arena zeroed
 		}
+		if (!CTL && lb && sif < SLB_N && wid == 0)
+			vec_load(gv, tv0); // issued here, evaluated after the packing
 #pragma unroll
 		for (uint32_t c = 0; c < ACH; c++) {
-			if (c < c0 || c >= c1)
+			if (c < c0 || c >= c1 || !data)
 				continue;
 			// opaque per pass: otherwise the table offsets of every chunk are
 			// hoisted out of the pass loop (~70 more VGPRs)
@@ -335,107 +471,29 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_
 			// keep the chunks' table lookups apart (hoisted, they cost ~80 VGPRs)
 			__builtin_amdgcn_sched_barrier(0);
 		}
-		__syncthreads(); // B3: the pass is packed
+		if (CTL && ctl && ps == 0)
+			evaluate(gv, tv0); // while the data waves pack
+		__syncthreads(); // B3: the pass is packed (CTL: and the frame offset is in LDS)
 		uint32_t pred_next = 0u; // (thread 0) the pass's last 32 bits, for the next pass
 		if (ps + 1u < npass && tid == 0) {
 			const uint32_t s0 = pbits - 32u, q = s0 >> 5, sh = s0 & 31u;
 			pred_next = sh ? (AR[q] << sh) | (AR[q + 1] >> (32u - sh)) : AR[q];
 		}
 		if (ps == 0) {
-			// ---- decoupled look-back (wave 0) ----------------------------
-			if (wid == 0) {
-				uint32_t Pw = HDR_BITS, prd = 0u;
-				if (is_first) {
-					// header bytes 20-21 (low half of the outlier field) share
-					// the first payload dword of the 22-byte header
-					prd = STREAM ? 0u : (cd.outlier & 0xFFFFu);
-				} else {
-					const bool slb = sif >= SLB_N;
-					if (slb) {
-						typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
-						auto sptr = [](const uint64_t *p) {
-							const uint64_t v = (uint64_t)(uintptr_t)p;
-							const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)v);
-							const uint32_t h = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-							return (const uint64_t *)(uintptr_t)(((uint64_t)h << 32) | l);
-						};
-						const uint64_t *gp = sptr(&a.agg[gseg - SLB_N]);
-						const uint64_t *tp = sptr(&a.tail[gseg - 1u]);
-						u32x16 q[2];
-						uint64_t tq;
-						asm volatile("s_load_dwordx16 %0, %3, 0x0 glc\n\t"
-							     "s_load_dwordx16 %1, %3, 0x40 glc\n\t"
-							     "s_load_dwordx2 %2, %4, 0x0 glc\n\t"
-							     "s_waitcnt lgkmcnt(0)"
-							     : "=&s"(q[0]), "=&s"(q[1]), "=&s"(tq)
-							     : "s"(gp), "s"(tp)
-							     : "memory");
-						// granule gseg - SLB_N + i -> lane SLB_N - 1 - i; lanes >= SLB_N
-						// read as unpublished (tag 0)
-						uint32_t vl = 0u, vh = 0u;
-#pragma unroll
-						for (uint32_t i = 0; i < SLB_N; i++) {
-							vl = lane == SLB_N - 1u - i ? q[i >> 3][2u * (i & 7u)] : vl;
-							vh = lane == SLB_N - 1u - i ? q[i >> 3][2u * (i & 7u) + 1u] : vh;
-						}
-						gv = ((uint64_t)vh << 32) | vl;
-						tv0 = tq;
-					}
-					uint32_t sum = 0u, spins = 0u;
-					int64_t j = (int64_t)gseg - 1;
-					for (;;) {
-						const int64_t idx = j - (int64_t)lane;
-						const bool inr = idx >= (int64_t)first_seg;
-						const uint32_t tag = (uint32_t)(gv >> 32);
-						const bool valid = inr && (tag >> 1) == a.epoch;
-						const bool incl = valid && (tag & 1u);
-						const uint64_t incl_m = __ballot(incl);
-						const uint64_t bad_m = __ballot(inr && !valid);
-						const uint32_t fi = incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
-						const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
-						if (bad_m & need) {
-							// a needed predecessor has not published: re-poll this window
-							if (++spins > AIRS_SPIN_LIMIT) {
-								if (lane == 0)
-									atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-								break;
-							}
-							__builtin_amdgcn_s_sleep(1);
-						} else {
-							sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv : 0u);
-							if (incl_m)
-								break;
-							j -= 64;
-						}
-						const int64_t id2 = j - (int64_t)lane;
-						gv = id2 >= (int64_t)first_seg ? gran_load(&a.agg[id2]) : 0ull;
-					}
-					Pw = sum;
-					if (lane == 0)
-						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (Pw + A));
-					if (lane == 0) {
-						uint64_t tv = tv0;
-						for (uint32_t sp = 0; (uint32_t)(tv >> 32) != a.epoch; sp++) {
-							if (sp > AIRS_SPIN_LIMIT) {
-								atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-								break;
-							}
-							__builtin_amdgcn_s_sleep(1);
-							tv = gran_load(&a.tail[gseg - 1u]);
-						}
-						prd = (uint32_t)tv;
-					}
+			if (!CTL) {
+				// ---- decoupled look-back (wave 0), after the packing --------
+				if (wid == 0) {
+					if (lb && sif >= SLB_N)
+						slb_load(gv, tv0, false);
+					evaluate(gv, tv0);
 				}
-				if (lane == 0) {
-					s_misc[1] = Pw;
-					s_misc[2] = prd;
-				}
+				__syncthreads(); // B4: the frame offset
 			}
-			__syncthreads(); // B4: the frame offset
 			P = __builtin_amdgcn_readfirstlane(s_misc[1]);
 			pred = s_misc[2];
 		}
-		store_image(P + pb0, pbits, pred, is_last && c1 == ACH);
+		if (data)
+			store_image(P + pb0, pbits, pred, is_last && c1 == ACH);
 		pred = pred_next;
 	}
 
@@ -503,19 +561,39 @@ bool arena_enabled()
 	return on != 0;
 }
 
+// AIRS_ARENA_CTL (env, A/B experiments): 1 = the control-wave form
+static bool arena_ctl()
+{
+	static int on = -1;
+	if (on < 0) {
+		const char *s = getenv("AIRS_ARENA_CTL");
+		on = s ? atoi(s) != 0 : AIRS_ARENA_CTL_DEFAULT;
+	}
+	return on != 0;
+}
+
+template <int PRE, bool STREAM>
+static void arena_go(const KArgs &k, uint32_t grid, size_t lds, hipStream_t s)
+{
+	if (arena_ctl())
+		hipLaunchKernelGGL((arena_kernel<PRE, STREAM, true>), dim3(grid), dim3(EWG + 64), lds, s, k);
+	else
+		hipLaunchKernelGGL((arena_kernel<PRE, STREAM, false>), dim3(grid), dim3(EWG), lds, s, k);
+}
+
 bool arena_encode(const KArgs &k, uint32_t pre, bool stream, uint32_t grid, hipStream_t s)
 {
 	const size_t lds = (size_t)(k.img_words + 4u) * 4u;
 	if (pre == PRE_DIFF) {
 		if (stream)
-			hipLaunchKernelGGL((arena_kernel<PRE_DIFF, true>), dim3(grid), dim3(EWG), lds, s, k);
+			arena_go<PRE_DIFF, true>(k, grid, lds, s);
 		else
-			hipLaunchKernelGGL((arena_kernel<PRE_DIFF, false>), dim3(grid), dim3(EWG), lds, s, k);
+			arena_go<PRE_DIFF, false>(k, grid, lds, s);
 	} else if (pre == PRE_NONE) {
 		if (stream)
-			hipLaunchKernelGGL((arena_kernel<PRE_NONE, true>), dim3(grid), dim3(EWG), lds, s, k);
+			arena_go<PRE_NONE, true>(k, grid, lds, s);
 		else
-			hipLaunchKernelGGL((arena_kernel<PRE_NONE, false>), dim3(grid), dim3(EWG), lds, s, k);
+			arena_go<PRE_NONE, false>(k, grid, lds, s);
 	} else {
 		return false;
 	}
