@@ -55,9 +55,39 @@ namespace airs {
 #ifndef AIRS_ARENA_CTL_DEFAULT     // the control-wave form (arena_kernel CTL)
 #define AIRS_ARENA_CTL_DEFAULT 0
 #endif
+#ifndef AIRS_ARENA_AUTO_DEFAULT    // AUTO launches take the arena kernel
+#define AIRS_ARENA_AUTO_DEFAULT 1
+#endif
 #ifndef AIRS_ARENA_WORDS_DEFAULT   // arena words: 6400 = 12.5 bits per sample, ~25 KiB of LDS
 #define AIRS_ARENA_WORDS_DEFAULT 6400u
 #endif
+
+// q = (m + 1) >> k of a pair of mapped values, packed.  v = m + 1 is formed
+// with a saturating add, so m = 65535 gives v = 65535 instead of 65536; below
+// k = 12 the clamps min(q, 16) / min(q, 17) hide that (q >= 31), from k = 12
+// on (AUTO frames only) the lost carry is added back: (65536 >> k) =
+// (65535 >> k) + 1 for every k >= 0.
+__device__ __forceinline__ u16x2 rice_q(uint32_t mpair, uint32_t k, bool big)
+{
+	const u16x2 vs = __builtin_elementwise_add_sat(pk(mpair), (u16x2)(1));
+	u16x2 q = vs >> (u16x2)((unsigned short)k);
+	if (big) {
+		const u16x2 vw = pk(mpair) + (u16x2)(1); // wraps to 0 for m = 65535
+		q += (vs - vw) >> (u16x2)(15);
+	}
+	return q;
+}
+
+// rice_table_entry (enc_common.h) for every k <= 15: T'[q] mod 2^32, so that
+// m + T'[q] is the codeword for q + k + 1 up to 32 bits (q <= 16 at k >= 12,
+// so the escape entry 17 is only reached for k <= 11)
+__device__ __forceinline__ uint2 rice_entry_any_k(uint32_t q, uint32_t k)
+{
+	if (q >= 17u)
+		return make_uint2(0u, k + 17u);
+	const uint64_t t = (1ull << (q + k + 1u)) - (2ull << k) - ((uint64_t)q << k) + 1ull;
+	return make_uint2((uint32_t)t, k + 1u + q);
+}
 
 // CTL: a fifth wave (the control wave) owns the look-back: it issues the
 // scalar granule loads before the packing starts (its barrier instruction
@@ -65,10 +95,18 @@ namespace airs {
 // frame offset in LDS by the barrier that ends the packing; the four data
 // waves never wait for the round trip.  Without CTL, wave 0 evaluates the
 // look-back after the packing.
-template <int PRE, bool STREAM, bool CTL>
+//
+// AUTO (CMP_GPU_AUTO_RICE, cfg3): the frame's Rice k is chosen from the
+// samples already in registers, as encode_kernel's fused selection does
+// (DESIGN.md 3.1.1): a 129-bin histogram of (floor(log2 v), next 3 bits) per
+// segment in the arena, the 16 candidate sums published as granules, the
+// frame's argmin; the same granules give each segment its exact frame offset,
+// so there is no look-back, only the predecessor's tail.
+template <int PRE, bool STREAM, bool CTL, bool AUTO>
 __global__ __launch_bounds__(EWG + (CTL ? 64 : 0)) __attribute__((amdgpu_waves_per_eu(AIRS_ARENA_WPE, 8))) void
 arena_kernel(KArgs a)
 {
+	static_assert(!AUTO || (!CTL && !STREAM), "AUTO: frames, no control wave");
 	static_assert(EPT == 16u, "lane t owns samples [16t, 16t+16) of a chunk");
 	constexpr uint32_t HDR_BITS = STREAM ? 0u : 176u; // 22-byte header (GOLOMB_ZERO)
 	constexpr uint32_t SLB_N = AIRS_ARENA_SLB_N;
@@ -88,10 +126,23 @@ arena_kernel(KArgs a)
 	const bool data = !ctl;
 	const uint32_t lbw = CTL ? EWG / 64 : 0u; // the wave that runs the look-back
 	// frame-interleaved dispatch (encode_kernel): consecutive blocks take the
-	// same segment index of consecutive frames
+	// same segment index of consecutive frames.  AUTO: frame-major and
+	// XCD-local instead (frame 8 j + x takes blocks x + 8 (j spf + s)), so a
+	// frame's segments, which wait for each other's candidates, are dispatched
+	// together on one XCD; the grid is padded to whole groups of 8 frames
 	const uint32_t seg = blockIdx.x;
 	const uint32_t nfr = a.num_segs / a.segs_per_frame;
-	const uint32_t sif = seg / nfr, lf = seg - sif * nfr;
+	uint32_t sif, lf;
+	if (AUTO) {
+		const uint32_t pq = seg >> 3;
+		sif = pq % a.segs_per_frame;
+		lf = 8u * (pq / a.segs_per_frame) + (seg & 7u);
+		if (lf >= nfr)
+			return; // padding block
+	} else {
+		sif = seg / nfr;
+		lf = seg - sif * nfr;
+	}
 	const uint32_t gseg = lf * a.segs_per_frame + sif;
 	const uint32_t frame =
 		__builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
@@ -116,10 +167,12 @@ arena_kernel(KArgs a)
 			prevld[c] = reinterpret_cast<const uint16_t *>(fsrc)[first - 1u];
 	}
 
-	const uint32_t g = __builtin_amdgcn_readfirstlane(a.frame_g ? a.frame_g[frame] : a.g);
-	const Coder cd = make_coder<ENC_ZERO>(g, a.outlier_param);
-	const uint32_t k = cd.k;
-	if (tid < 18u)
+	// (AUTO: set once the frame's k is chosen)
+	uint32_t g = AUTO ? 1u : __builtin_amdgcn_readfirstlane(a.frame_g ? a.frame_g[frame] : a.g);
+	Coder cd = make_coder<ENC_ZERO>(g, a.outlier_param);
+	uint32_t k = cd.k;
+	bool big = false; // k >= 12 (AUTO only): rice_q's exact carry
+	if (!AUTO && tid < 18u)
 		s_rice[tid] = rice_table_entry(tid, k);
 
 	// ---- phase 1: residuals, mapped values, code lengths (packed 16-bit) ---
@@ -151,14 +204,179 @@ arena_kernel(KArgs a)
 			if (PRE == PRE_DIFF)
 				u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
 			mp[c][j] = zigzag_pk(u);
-			const u16x2 v = __builtin_elementwise_add_sat(pk(mp[c][j]), (u16x2)(1));
-			acc += __builtin_elementwise_min(v >> (u16x2)((unsigned short)k), (u16x2)(16));
+			if (!AUTO)
+				acc += __builtin_elementwise_min(rice_q(mp[c][j], k, false), (u16x2)(16));
 		}
 		T[c] = EPT * (k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
 		// opaque: the packer recomputes from mp, not from phase 1's temporaries
 #pragma unroll
 		for (uint32_t i = 0; i < EPT / 2; i++)
 			asm volatile("" : "+v"(mp[c][i]));
+	}
+
+	uint32_t auto_P = 0u; // AUTO: the segment's frame bit offset (header included)
+	if constexpr (AUTO) {
+		// ---- the frame's Rice k ---------------------------
+		// 1. histogram: one 32-bit counter per (bin, lane mod 32) in the arena;
+		// lanes l and l + 32 share a counter but sit in different LDS lane
+		// groups, so the atomics (no return) are conflict-free
+		__shared__ uint32_t s_hist[AUTO_BINS];
+		__shared__ uint32_t s_kt[EWG / 64][16];
+		uint32_t *const H = AR;
+		{
+			uint4 *Z = reinterpret_cast<uint4 *>(H);
+			for (uint32_t i = tid; i < AUTO_BINS * 32u / 4u; i += EWG)
+				Z[i] = make_uint4(0u, 0u, 0u, 0u);
+		}
+		// this lane's counter of bin b is at byte hbase + 128 (b + 1016)
+		const uint32_t hbase = (uint32_t)(uintptr_t)H + 4u * (lane & 31u) - 1016u * 128u;
+		__syncthreads();
+#pragma unroll
+		for (uint32_t c = 0; c < ACH; c++) {
+#pragma unroll
+			for (uint32_t jp = 0; jp < EPT / 2; jp++) {
+				// an opaque copy: otherwise the bins are computed ahead of the
+				// barrier above (~150 more VGPRs)
+				uint32_t wv = mp[c][jp];
+				asm volatile("" : "+v"(wv));
+#pragma unroll
+				for (uint32_t h = 0; h < 2; h++) {
+					const uint32_t v = half16(wv, h) + 1u;
+					// bin + 1016 = the top 12 bits of the float v
+					uint32_t ha;
+					asm("v_bfe_u32 %0, %1, 20, 12\n\tv_lshl_add_u32 %0, %0, 7, %2"
+					    : "=&v"(ha)
+					    : "v"(__float_as_uint((float)v)), "v"(hbase));
+					__hip_atomic_fetch_add(reinterpret_cast<lds_u32 *>((uintptr_t)ha), 1u, __ATOMIC_RELAXED,
+							       __HIP_MEMORY_SCOPE_WORKGROUP);
+				}
+			}
+		}
+		__syncthreads();
+		// 2. bin totals: threads 2r, 2r + 1 sum the halves of row r < 128
+		// (four 16-byte reads each); wave 0 sums row 128 (v = 65536)
+		{
+			const uint32_t r = tid >> 1, hh = tid & 1u;
+			const uint4 *row = reinterpret_cast<const uint4 *>(H + r * 32u + hh * 16u);
+			uint32_t sm = 0u;
+#pragma unroll
+			for (uint32_t q = 0; q < 4u; q++) {
+				const uint4 x = row[(q + r) & 3u];
+				sm += x.x + x.y + x.z + x.w;
+			}
+			sm += __shfl_xor(sm, 1, 64);
+			if (hh == 0u)
+				s_hist[r] = sm;
+			static_assert(AUTO_BINS == EWG / 2u + 1u, "rows 0..127 by thread pairs, then row 128");
+			if (wid == 0) {
+				const uint32_t s128 = wave_sum(lane < 32u ? H[128u * 32u + lane] : 0u);
+				if (lane == 0)
+					s_hist[128] = s128;
+			}
+		}
+		__syncthreads();
+		// 3. this segment's 16 candidate sums: thread (slice sl, k) covers
+		// bins sl, sl + 16, ...; the four slices of a wave meet by shuffles
+		{
+			const uint32_t kk = tid & 15u, sl = tid >> 4;
+			uint32_t part = 0u;
+#pragma unroll
+			for (uint32_t i = 0; i < (AUTO_BINS + 15u) / 16u; i++) {
+				const uint32_t b = sl + 16u * i;
+				if (b < AUTO_BINS) {
+					// min(v >> kk, 16) of every v in bin b (encode_kernel auto_term)
+					const uint32_t t = b >> 3, top4 = 8u + (b & 7u);
+					const uint32_t term = kk + 4u <= t ? 16u : kk > t ? 0u : top4 >> (kk + 3u - t);
+					part += s_hist[b] * term;
+				}
+			}
+			part += __shfl_xor(part, 16, 64);
+			part += __shfl_xor(part, 32, 64);
+			if (lane < 16u)
+				s_kt[wid][kk] = part;
+		}
+		__syncthreads();
+		if (wid == 0) {
+			// 4. publish (lanes 0-15), then read the frame's 16 spf granules
+			if (lane < 16u) {
+				const uint32_t sk = s_kt[0][lane] + s_kt[1][lane] + s_kt[2][lane] + s_kt[3][lane];
+				gran_store(&a.ktot[(uint64_t)gseg * 16u + lane], ((uint64_t)a.epoch << 32) | sk);
+			}
+			const uint32_t fs = gseg - sif, ng = a.segs_per_frame * 16u;
+			constexpr uint32_t NL = (AUTO_MAX_SPF + 3u) / 4u; // granule loads per lane
+			uint64_t gk[NL];
+#pragma unroll
+			for (uint32_t i = 0; i < NL; i++) {
+				const uint32_t gi = 64u * i + lane;
+				gk[i] = gran_load(&a.ktot[(uint64_t)fs * 16u + (gi < ng ? gi : 0u)]);
+			}
+			for (uint32_t spins = 0;;) {
+				bool bad = false;
+#pragma unroll
+				for (uint32_t i = 0; i < NL; i++)
+					bad |= 64u * i + lane < ng && (uint32_t)(gk[i] >> 32) != a.epoch;
+				if (!__ballot(bad))
+					break;
+				if (++spins > AIRS_SPIN_LIMIT) {
+					if (lane == 0)
+						atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+					break;
+				}
+				__builtin_amdgcn_s_sleep(1);
+#pragma unroll
+				for (uint32_t i = 0; i < NL; i++) {
+					const uint32_t gi = 64u * i + lane;
+					if (gi < ng && (uint32_t)(gk[i] >> 32) != a.epoch)
+						gk[i] = gran_load(&a.ktot[(uint64_t)fs * 16u + gi]);
+				}
+			}
+			// lane l holds segment 4 i + l / 16, candidate k = l % 16
+			uint32_t tot = 0u, pre = 0u;
+#pragma unroll
+			for (uint32_t i = 0; i < NL; i++) {
+				const uint32_t gi = 64u * i + lane;
+				const uint32_t v = gi < ng ? (uint32_t)gk[i] : 0u;
+				tot += v;
+				pre += (gi >> 4) < sif ? v : 0u;
+			}
+			tot += __shfl_xor(tot, 16, 64);
+			tot += __shfl_xor(tot, 32, 64);
+			pre += __shfl_xor(pre, 16, 64);
+			pre += __shfl_xor(pre, 32, 64);
+			const uint32_t kk = lane & 15u;
+			// frame bits for k (< 2^28: spf <= 32 segments), ties to the smaller k
+			uint32_t key = ((tot + n * (kk + 1u)) << 4) | kk;
+#pragma unroll
+			for (uint32_t d = 1; d < 16u; d <<= 1)
+				key = min(key, (uint32_t)__shfl_xor(key, d, 64));
+			const uint32_t ks = key & 15u;
+			const uint32_t pre_k = __shfl(pre, ks, 64);
+			if (lane == 0) {
+				s_misc[0] = ks;
+				// every segment before this one is whole
+				s_misc[3] = HDR_BITS + pre_k + sif * ASEGN * (ks + 1u);
+			}
+		}
+		__syncthreads();
+		k = __builtin_amdgcn_readfirstlane(s_misc[0]);
+		auto_P = __builtin_amdgcn_readfirstlane(s_misc[3]);
+		g = 1u << k;
+		cd = make_coder<ENC_ZERO>(g, a.outlier_param);
+		big = k >= 12u;
+		if (tid < 18u)
+			s_rice[tid] = rice_entry_any_k(tid, k);
+		// the code lengths, now that k is known
+#pragma unroll
+		for (uint32_t c = 0; c < ACH; c++) {
+			u16x2 acc = (u16x2)(0);
+#pragma unroll
+			for (uint32_t j = 0; j < EPT / 2; j++)
+				acc += __builtin_elementwise_min(rice_q(mp[c][j], k, big), (u16x2)(16));
+			T[c] = EPT * (k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
+#pragma unroll
+			for (uint32_t i = 0; i < EPT / 2; i++)
+				asm volatile("" : "+v"(mp[c][i]));
+		}
 	}
 
 	// ---- per-chunk block scans (DPP within waves, LDS across waves) -------
@@ -187,7 +405,7 @@ arena_kernel(KArgs a)
 	}
 	base[ACH] = A;
 	const uint32_t first_seg = gseg - sif;
-	if (wid == lbw && lane == 0) {
+	if (!AUTO && wid == lbw && lane == 0) {
 		const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
 		gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
 	}
@@ -201,9 +419,8 @@ arena_kernel(KArgs a)
 		for (uint32_t j = 0; j < EPT / 2; j++) {
 			if (j < EPT / 4 && k >= 3u)
 				continue;
-			const u16x2 v = __builtin_elementwise_add_sat(pk(mp[ACH - 1][j]), (u16x2)(1));
 			const uint32_t qa =
-				unpk(__builtin_elementwise_min(v >> (u16x2)((unsigned short)k), (u16x2)(17)) << (u16x2)(3));
+				unpk(__builtin_elementwise_min(rice_q(mp[ACH - 1][j], k, big), (u16x2)(17)) << (u16x2)(3));
 #pragma unroll
 			for (uint32_t h = 0; h < 2; h++) {
 				const uint2 e = *reinterpret_cast<const uint2 *>(tab + half16(qa, h));
@@ -331,6 +548,20 @@ arena_kernel(KArgs a)
 			// header bytes 20-21 (low half of the outlier field) share the
 			// first payload dword of the 22-byte header
 			prd = STREAM ? 0u : (cd.outlier & 0xFFFFu);
+		} else if (AUTO) {
+			Pw = auto_P; // from the frame's candidate granules
+			if (lane == 0) {
+				uint64_t tv = tv0;
+				for (uint32_t sp = 0; (uint32_t)(tv >> 32) != a.epoch; sp++) {
+					if (sp > AIRS_SPIN_LIMIT) {
+						atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+						break;
+					}
+					__builtin_amdgcn_s_sleep(1);
+					tv = gran_load(&a.tail[gseg - 1u]);
+				}
+				prd = (uint32_t)tv;
+			}
 		} else {
 			uint32_t sum = 0u, spins = 0u;
 			int64_t j = (int64_t)gseg - 1;
@@ -420,7 +651,9 @@ arena_kernel(KArgs a)
 		} else {
 			__syncthreads(); // B2: arena zeroed
 		}
-		if (!CTL && lb && sif < SLB_N && wid == 0)
+		if (!CTL && lb && AUTO && wid == 0)
+			tv0 = gran_load(&a.tail[gseg - 1u]); // AUTO: only the predecessor's tail
+		else if (!CTL && lb && sif < SLB_N && wid == 0)
 			vec_load(gv, tv0); // issued here, evaluated after the packing
 #pragma unroll
 		for (uint32_t c = 0; c < ACH; c++) {
@@ -439,9 +672,8 @@ arena_kernel(KArgs a)
 #pragma unroll
 				for (uint32_t jj = 0; jj < EPT / 4; jj++) {
 					const uint32_t j = hb * (EPT / 4) + jj;
-					const u16x2 v = __builtin_elementwise_add_sat(pk(mp[c][j]), (u16x2)(1));
-					const uint32_t qa = unpk(__builtin_elementwise_min(v >> (u16x2)((unsigned short)k), (u16x2)(17))
-								 << (u16x2)(3));
+					const uint32_t qa =
+						unpk(__builtin_elementwise_min(rice_q(mp[c][j], k, big), (u16x2)(17)) << (u16x2)(3));
 #pragma unroll
 					for (uint32_t h = 0; h < 2; h++)
 						te[2 * jj + h] = *reinterpret_cast<const uint2 *>(tab + half16(qa, h));
@@ -483,7 +715,7 @@ arena_kernel(KArgs a)
 			if (!CTL) {
 				// ---- decoupled look-back (wave 0), after the packing --------
 				if (wid == 0) {
-					if (lb && sif >= SLB_N)
+					if (!AUTO && lb && sif >= SLB_N)
 						slb_load(gv, tv0, false);
 					evaluate(gv, tv0);
 				}
@@ -576,9 +808,33 @@ template <int PRE, bool STREAM>
 static void arena_go(const KArgs &k, uint32_t grid, size_t lds, hipStream_t s)
 {
 	if (arena_ctl())
-		hipLaunchKernelGGL((arena_kernel<PRE, STREAM, true>), dim3(grid), dim3(EWG + 64), lds, s, k);
+		hipLaunchKernelGGL((arena_kernel<PRE, STREAM, true, false>), dim3(grid), dim3(EWG + 64), lds, s, k);
 	else
-		hipLaunchKernelGGL((arena_kernel<PRE, STREAM, false>), dim3(grid), dim3(EWG), lds, s, k);
+		hipLaunchKernelGGL((arena_kernel<PRE, STREAM, false, false>), dim3(grid), dim3(EWG), lds, s, k);
+}
+
+// AUTO launches (k.ktot set; grid padded to whole groups of 8 frames)
+bool arena_auto_encode(const KArgs &k, uint32_t pre, uint32_t grid, hipStream_t s)
+{
+	const size_t lds = (size_t)(k.img_words + 4u) * 4u;
+	if (pre == PRE_DIFF)
+		hipLaunchKernelGGL((arena_kernel<PRE_DIFF, false, false, true>), dim3(grid), dim3(EWG), lds, s, k);
+	else if (pre == PRE_NONE)
+		hipLaunchKernelGGL((arena_kernel<PRE_NONE, false, false, true>), dim3(grid), dim3(EWG), lds, s, k);
+	else
+		return false;
+	return true;
+}
+
+// AIRS_ARENA_AUTO=0 (env, A/B experiments) keeps AUTO launches on encode_kernel
+bool arena_auto_enabled()
+{
+	static int on = -1;
+	if (on < 0) {
+		const char *e = getenv("AIRS_ARENA_AUTO");
+		on = e ? atoi(e) != 0 : AIRS_ARENA_AUTO_DEFAULT;
+	}
+	return on != 0 && arena_enabled();
 }
 
 bool arena_encode(const KArgs &k, uint32_t pre, bool stream, uint32_t grid, hipStream_t s)

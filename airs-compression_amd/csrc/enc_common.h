@@ -491,6 +491,10 @@ uint32_t walk_ctx_samples();
 bool arena_encode(const KArgs &k, uint32_t pre, bool stream, uint32_t grid, hipStream_t s);
 uint32_t arena_words();
 bool arena_enabled();
+// AUTO (fused per-frame Rice k) launches of frames of whole 16 Ki-sample
+// segments, 16-bit NONE/DIFF: grid padded to whole groups of 8 frames
+bool arena_auto_encode(const KArgs &k, uint32_t pre, uint32_t grid, hipStream_t s);
+bool arena_auto_enabled();
 void stream_encode(const KArgs &k, uint32_t sample_bytes, uint32_t pre, uint32_t enc, bool rice, bool full,
 		   uint32_t grid, hipStream_t s);
 

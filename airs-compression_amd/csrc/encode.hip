@@ -1135,6 +1135,12 @@ template <int W, int PRE, int ENC, bool RICE, int MODEL>
 static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t s)
 {
 	if constexpr (ENC == ENC_ZERO && RICE && MODEL == 0 && (PRE == PRE_NONE || PRE == PRE_DIFF)) {
+		if (k.ktot && W == 2 && full && arena_auto_enabled()) { // fused Rice selection, the arena kernel
+			KArgs ka = k;
+			ka.img_words = arena_words();
+			arena_auto_encode(ka, PRE, grid, s);
+			return;
+		}
 		if (k.ktot) { // fused per-frame Rice selection (frame barrier: never persistent)
 			size_t lds = (size_t)2u * (k.img_words + 4u) * 4u; // two images (enc_kernel.h NIMG)
 			lds = lds > AUTO_BINS * 64u * 4u ? lds : AUTO_BINS * 64u * 4u; // the histogram

@@ -521,20 +521,28 @@ def main():
     ms_step = wall_max / args.steps * 1e3
     traffic, traffic_src = measured_traffic(wname)
     achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
+    ctl = os.environ.get("AIRS_ARENA_CTL", "0") not in ("", "0")
+    arena = ("airs::arena_kernel<DIFF,%s,%s> (enc_arena.hip: the Rice/ZERO fast path, one LDS arena per 16 Ki-sample "
+             "segment%s)" % ("STREAM" if wname == "cfg2s" else "frames", "CTL" if ctl else "-",
+                             ", a control wave runs the look-back" if ctl else ""))
+    if os.environ.get("AIRS_ARENA", "1") == "0":
+        arena = "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL> (AIRS_ARENA=0)"
     kernels = {
-        "cfg2": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL> (u16, DIFF, GOLOMB_ZERO, Rice): one launch per step",
-        "cfg2s": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,-,STREAM>: one launch per step, one look-back chain "
-                 "of 4096 segments",
-        "cfg3": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO> (the per-frame Rice k chosen in-kernel): one "
-                "launch per step",
-        "cfg4": "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL>: one launch per step",
+        "cfg2": arena + ": one launch per step",
+        "cfg2s": arena + ": one launch per step, one look-back chain of 4096 segments",
+        "cfg3": ("airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO>" if os.environ.get("AIRS_ARENA_AUTO") == "0" or
+                 os.environ.get("AIRS_ARENA") == "0" else "airs::arena_kernel<DIFF,frames,-,AUTO>") +
+                " (the per-frame Rice k chosen in-kernel from a histogram of the samples in registers): one launch "
+                "per step",
+        "cfg4": arena + ": one launch per step",
         "cfg5": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> (enc_walk.hip): ONE launch per step, one "
                 "1024-thread workgroup per stream walks its 16 acquisitions, the model in registers",
         "cfg5s8": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice> (enc_walk.hip, the segment walk): ONE launch per "
                   "step, a 320-thread workgroup per (stream, 4096-sample segment) walks the 16 acquisitions, each "
                   "acquisition's look-back resolved one step later",
-        "cfg5fb": "per acquisition: fb_step_kernel + fb_copy_kernel + encode_kernel<4,DIFF,ZERO,Rice,STORE> + "
-                  "encode_kernel<4,MODEL,MULTI,Rice,UPDATE> (frame-list holes)",
+        "cfg5fb": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> with the uncompressed fallback resolved on "
+                  "the chip: ONE launch per step, then one read-back of the draw counts and the identifier patch "
+                  "(patch_ids_kernel)",
     }
     result = None
     if rank == 0:

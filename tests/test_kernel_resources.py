@@ -21,12 +21,14 @@ LIB = os.path.join(PKG_DIR, "lib", "libairscmp.so")
 BUDGETS = {
     # cfg2 / cfg4: the arena kernel, DIFF and NONE, frames (5 waves per SIMD);
     # and its control-wave form (AIRS_ARENA_CTL)
-    "_ZN4airs12arena_kernelILi1ELb0ELb0EEEvNS_5KArgsE": (96, 17),
-    "_ZN4airs12arena_kernelILi0ELb0ELb0EEEvNS_5KArgsE": (96, 17),
-    "_ZN4airs12arena_kernelILi1ELb0ELb1EEEvNS_5KArgsE": (96, 28),
+    "_ZN4airs12arena_kernelILi1ELb0ELb0ELb0EEEvNS_5KArgsE": (96, 17),
+    "_ZN4airs12arena_kernelILi0ELb0ELb0ELb0EEEvNS_5KArgsE": (96, 17),
+    "_ZN4airs12arena_kernelILi1ELb0ELb1ELb0EEEvNS_5KArgsE": (96, 28),
+    # cfg3: the arena kernel with the fused per-frame Rice selection
+    "_ZN4airs12arena_kernelILi1ELb0ELb0ELb1EEEvNS_5KArgsE": (96, 0),
     # encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>: AIRS_ARENA=0 and the other shapes
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb0EEEvNS_5KArgsE": (128, 13),
-    # cfg3: the fused per-frame Rice selection
+    # encode_kernel's fused per-frame Rice selection (AIRS_ARENA_AUTO=0, partial segments)
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb1ELb0EEEvNS_5KArgsE": (128, 0),
     # cfg2s: payload-only stream
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb1EEEvNS_5KArgsE": (128, 0),
