@@ -5,9 +5,14 @@
 // lib/compress/cmp.c:296-312: NONE/DIFF residual (preprocess.c:268-300),
 // ZigZag (encoder.c:274-286), Golomb ZERO with g = 2^k (encoder.c:327-351,
 // zero escape :340-346), big-endian bit packing (bitstream_writer.h:124-158),
-// flush (:205-227), header (header.c:24-67).  Used for launches with 16-bit
+// flush (:205-227), header (header.c:24-67).  Eligible: launches with 16-bit
 // samples, NONE or DIFF, GOLOMB_ZERO with a power-of-two g <= 2048, no model,
-// whole 16 Ki-sample segments and 16-byte aligned frames (cfg2, cfg4).
+// whole 16 Ki-sample segments and 16-byte aligned frames (cfg2, cfg3, cfg4).
+//
+// AN EXPERIMENT, OFF BY DEFAULT (AIRS_ARENA=1 turns it on): measured on MI355X
+// it is 4-14 % slower than encode_kernel on cfg2, cfg3 and cfg4 in every form
+// below (the recomputed table offsets cost more VALU time than
+// the barriers and LDS it saves).  Kept bit-exact and tested (test_gpu_arena).
 //
 // What differs from encode_kernel is where a segment's bits wait for its
 // frame offset.  encode_kernel packs chunk by chunk into three rotating chunk
@@ -49,14 +54,17 @@ namespace airs {
 #ifndef AIRS_PRIO_ARENA            // phase-2 issue priority (encode_kernel AIRS_PRIO_P2)
 #define AIRS_PRIO_ARENA 1
 #endif
-#ifndef AIRS_ARENA_DEFAULT         // eligible launches take the arena kernel
-#define AIRS_ARENA_DEFAULT 1
+#ifndef AIRS_ARENA_DEFAULT         // eligible launches take the arena kernel (measured slower: off)
+#define AIRS_ARENA_DEFAULT 0
 #endif
 #ifndef AIRS_ARENA_CTL_DEFAULT     // the control-wave form (arena_kernel CTL)
 #define AIRS_ARENA_CTL_DEFAULT 0
 #endif
-#ifndef AIRS_ARENA_AUTO_DEFAULT    // AUTO launches take the arena kernel
+#ifndef AIRS_ARENA_AUTO_DEFAULT    // AUTO launches take the arena kernel (with AIRS_ARENA)
 #define AIRS_ARENA_AUTO_DEFAULT 1
+#endif
+#ifndef AIRS_ARENA_KEEPQ
+#define AIRS_ARENA_KEEPQ 0
 #endif
 #ifndef AIRS_ARENA_WORDS_DEFAULT   // arena words: 6400 = 12.5 bits per sample, ~25 KiB of LDS
 #define AIRS_ARENA_WORDS_DEFAULT 6400u
@@ -177,6 +185,10 @@ arena_kernel(KArgs a)
 
 	// ---- phase 1: residuals, mapped values, code lengths (packed 16-bit) ---
 	uint32_t mp[ACH][EPT / 2]; // mapped values, two per register
+	// AIRS_ARENA_KEEPQ (experiment): the table offsets 8 min(q, 17) kept from
+	// the lengths pass (encode_kernel AIRS_KEEP_Q) instead of recomputed
+	constexpr bool KQ = AIRS_ARENA_KEEPQ != 0;
+	uint32_t mq[KQ ? ACH : 1][EPT / 2];
 	uint32_t T[ACH];           // this lane's bits in chunk c
 #pragma unroll
 	for (uint32_t c = 0; c < ACH; c++) {
@@ -204,14 +216,21 @@ arena_kernel(KArgs a)
 			if (PRE == PRE_DIFF)
 				u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
 			mp[c][j] = zigzag_pk(u);
-			if (!AUTO)
-				acc += __builtin_elementwise_min(rice_q(mp[c][j], k, false), (u16x2)(16));
+			if (!AUTO) {
+				const u16x2 q = rice_q(mp[c][j], k, false);
+				acc += __builtin_elementwise_min(q, (u16x2)(16));
+				if (KQ)
+					mq[KQ ? c : 0][j] = unpk(__builtin_elementwise_min(q, (u16x2)(17)) << (u16x2)(3));
+			}
 		}
 		T[c] = EPT * (k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
 		// opaque: the packer recomputes from mp, not from phase 1's temporaries
 #pragma unroll
-		for (uint32_t i = 0; i < EPT / 2; i++)
+		for (uint32_t i = 0; i < EPT / 2; i++) {
 			asm volatile("" : "+v"(mp[c][i]));
+			if (KQ)
+				asm volatile("" : "+v"(mq[KQ ? c : 0][i]));
+		}
 	}
 
 	uint32_t auto_P = 0u; // AUTO: the segment's frame bit offset (header included)
@@ -370,12 +389,19 @@ arena_kernel(KArgs a)
 		for (uint32_t c = 0; c < ACH; c++) {
 			u16x2 acc = (u16x2)(0);
 #pragma unroll
-			for (uint32_t j = 0; j < EPT / 2; j++)
-				acc += __builtin_elementwise_min(rice_q(mp[c][j], k, big), (u16x2)(16));
+			for (uint32_t j = 0; j < EPT / 2; j++) {
+				const u16x2 q = rice_q(mp[c][j], k, big);
+				acc += __builtin_elementwise_min(q, (u16x2)(16));
+				if (KQ)
+					mq[KQ ? c : 0][j] = unpk(__builtin_elementwise_min(q, (u16x2)(17)) << (u16x2)(3));
+			}
 			T[c] = EPT * (k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
 #pragma unroll
-			for (uint32_t i = 0; i < EPT / 2; i++)
+			for (uint32_t i = 0; i < EPT / 2; i++) {
 				asm volatile("" : "+v"(mp[c][i]));
+				if (KQ)
+					asm volatile("" : "+v"(mq[KQ ? c : 0][i]));
+			}
 		}
 	}
 
@@ -662,8 +688,11 @@ arena_kernel(KArgs a)
 			// opaque per pass: otherwise the table offsets of every chunk are
 			// hoisted out of the pass loop (~70 more VGPRs)
 #pragma unroll
-			for (uint32_t i = 0; i < EPT / 2; i++)
+			for (uint32_t i = 0; i < EPT / 2; i++) {
 				asm volatile("" : "+v"(mp[c][i]));
+				if (KQ)
+					asm volatile("" : "+v"(mq[KQ ? c : 0][i]));
+			}
 			Packer pk1;
 			pk1.init(AR, base[c] - pb0 + excl[c]);
 #pragma unroll
@@ -673,7 +702,8 @@ arena_kernel(KArgs a)
 				for (uint32_t jj = 0; jj < EPT / 4; jj++) {
 					const uint32_t j = hb * (EPT / 4) + jj;
 					const uint32_t qa =
-						unpk(__builtin_elementwise_min(rice_q(mp[c][j], k, big), (u16x2)(17)) << (u16x2)(3));
+						KQ ? mq[KQ ? c : 0][j]
+						   : unpk(__builtin_elementwise_min(rice_q(mp[c][j], k, big), (u16x2)(17)) << (u16x2)(3));
 #pragma unroll
 					for (uint32_t h = 0; h < 2; h++)
 						te[2 * jj + h] = *reinterpret_cast<const uint2 *>(tab + half16(qa, h));
@@ -781,16 +811,13 @@ uint32_t arena_words()
 	return w;
 }
 
-// AIRS_ARENA=0 (env, A/B experiments) sends the eligible launches back to
-// encode_kernel
+// AIRS_ARENA=1 (env, read at every launch: A/B experiments and the arena's
+// parity tests) sends the eligible launches to the arena kernel; measured
+// slower than encode_kernel on every workload, so off by default
 bool arena_enabled()
 {
-	static int on = -1;
-	if (on < 0) {
-		const char *s = getenv("AIRS_ARENA");
-		on = s ? atoi(s) != 0 : AIRS_ARENA_DEFAULT;
-	}
-	return on != 0;
+	const char *s = getenv("AIRS_ARENA");
+	return s ? atoi(s) != 0 : AIRS_ARENA_DEFAULT != 0;
 }
 
 // AIRS_ARENA_CTL (env, A/B experiments): 1 = the control-wave form
@@ -829,12 +856,8 @@ bool arena_auto_encode(const KArgs &k, uint32_t pre, uint32_t grid, hipStream_t 
 // AIRS_ARENA_AUTO=0 (env, A/B experiments) keeps AUTO launches on encode_kernel
 bool arena_auto_enabled()
 {
-	static int on = -1;
-	if (on < 0) {
-		const char *e = getenv("AIRS_ARENA_AUTO");
-		on = e ? atoi(e) != 0 : AIRS_ARENA_AUTO_DEFAULT;
-	}
-	return on != 0 && arena_enabled();
+	const char *e = getenv("AIRS_ARENA_AUTO");
+	return (e ? atoi(e) != 0 : AIRS_ARENA_AUTO_DEFAULT != 0) && arena_enabled();
 }
 
 bool arena_encode(const KArgs &k, uint32_t pre, bool stream, uint32_t grid, hipStream_t s)

@@ -123,7 +123,10 @@ __device__ __forceinline__ u32x4 rsrc_words(const void *base, uint32_t bytes)
 // for every store and for the prefetch of the step after).
 __device__ __forceinline__ void store_b128_nc(u32x4 v, uint32_t byte_off, u32x4 rsrc)
 {
-	asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen" ::"v"(v), "v"(byte_off), "s"(rsrc) : "memory");
+	// s_nop 1: a VALU write of the data registers right after a store of more
+	// than 64 bits needs wait states, and hipcc does not pad after inline asm
+	// (seen: the next address computed into v[18:19] was stored as sample data)
+	asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" ::"v"(v), "v"(byte_off), "s"(rsrc) : "memory");
 }
 
 __device__ __forceinline__ void store_b32_nc(uint32_t v, uint32_t byte_off, u32x4 rsrc)
@@ -245,18 +248,25 @@ __device__ __forceinline__ uint32_t hdr_bits(int pre, int enc)
 	return (pre == PRE_NONE && enc == ENC_RAW) ? 128u : 176u;
 }
 
-template <int W, int PRE_P, int ENC_P, bool RICE_P, int ENC_S, bool RICE_S>
-__global__ __launch_bounds__(320) void walk_kernel(WArgs a)
+// DW data waves (2 or 4) and one control wave: a segment is DW * 1024
+// samples.  Two data waves double the workgroups of a batch, for batches of
+// few contexts (configs[4]'s 32 streams per GPU at N = 8: 1024 workgroups
+// instead of 512, four per CU instead of two).
+template <int W, int PRE_P, int ENC_P, bool RICE_P, int ENC_S, bool RICE_S, int DW>
+__global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 {
+	static_assert(DW == 2 || DW == 4, "two or four data waves");
 	constexpr uint32_t RW = EPT * W / 16u; // uint4 per lane
+	constexpr uint32_t NT = 64u * (DW + 1u), ND = 64u * DW; // threads, data threads
+	constexpr uint32_t SEGW = ND * EPT;                      // samples per segment
 	extern __shared__ __attribute__((aligned(16))) uint32_t L_img[];
-	__shared__ uint32_t s_wsum[4];
+	__shared__ uint32_t s_wsum[DW];
 	__shared__ uint32_t s_ctl[4];
 	__shared__ __attribute__((aligned(16))) uint2 s_tab[2][WTAB];
 
 	const uint32_t tid = threadIdx.x, lane = tid & 63u;
 	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-	const bool data = wid < 4u;
+	const bool data = wid < DW;
 	// logical block index from a ticket taken at start: every
 	// workgroup with a smaller index has started (is resident or done), so a
 	// look-back only ever waits on a workgroup that is running, whatever order
@@ -268,7 +278,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 	const uint32_t c = lb / a.spf, j = lb - c * a.spf;
 	const bool is_first = j == 0u, is_last = j + 1u == a.spf;
 	const uint32_t n = a.n;
-	const uint32_t first = j * AIRS_SEG + (data ? tid : 0u) * EPT; // lane's first sample
+	const uint32_t first = j * SEGW + (data ? tid : 0u) * EPT; // lane's first sample
 	uint16_t *mbase = reinterpret_cast<uint16_t *>(a.model_ptrs ? (uint8_t *)(uintptr_t)a.model_ptrs[c]
 								    : a.model + (uint64_t)c * a.model_stride);
 	// two images (a.img_words each, after a 4-word pad): acquisition a packs
@@ -286,7 +296,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		if (fast_s)
 			s_tab[1][tid] = walk_table_entry<ENC_S>(tid, cs);
 	}
-	for (uint32_t i = tid; i < 2u * a.img_words + 8u; i += 320u)
+	for (uint32_t i = tid; i < 2u * a.img_words + 8u; i += NT)
 		L_img[i] = 0u;
 
 	const uint32_t seq0 = a.seq0s ? a.seq0s[c] : a.seq0;
@@ -409,19 +419,25 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 			excl = inc - T;
 		}
 		lds_barrier(); // B1: wave totals
-		const uint32_t w0 = s_wsum[0], w1 = s_wsum[1], w2 = s_wsum[2], w3 = s_wsum[3];
-		const uint32_t A = have ? __builtin_amdgcn_readfirstlane(w0 + w1 + w2 + w3) : 0u;
+		uint32_t Asum = 0u, wpre = 0u;
+#pragma unroll
+		for (uint32_t w = 0; w < DW; w++) {
+			const uint32_t v = s_wsum[w];
+			wpre += w < wid ? v : 0u;
+			Asum += v;
+		}
+		const uint32_t A = have ? __builtin_amdgcn_readfirstlane(Asum) : 0u;
 		if (wid == 0u)
 			wstamp(a, acq < a.fpc ? acq : a.fpc - 1u, 1u);
 		if (data) {
 			if (have) {
-				excl += (wid > 0u ? w0 : 0u) + (wid > 1u ? w1 : 0u) + (wid > 2u ? w2 : 0u);
+				excl += wpre;
 				// ---- pack into this acquisition's image -------------------------
 				if (prim)
 					walk_pack<ENC_P, RICE_P>(img, excl, mp, oq, cp, fast_p, tab_p);
 				else
 					walk_pack<ENC_S, RICE_S>(img, excl, mp, oq, cs, fast_s, tab_s);
-				if (wid == 3u && !is_last) {
+				if (wid == DW - 1u && !is_last) {
 					// the segment's last 32 bits (wave 3's own lanes wrote them) for
 					// the successor's first word (read by it one step later)
 					asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -517,7 +533,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 				// ---- store: funnel shift to the frame bit offset, big-endian ------
 				const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)imgp);
 				const uint32_t nquad = nfull >> 2;
-				for (uint32_t p = tid; p < nquad; p += 256u) {
+				for (uint32_t p = tid; p < nquad; p += ND) {
 					const uint32_t jw = 4u * p;
 					const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + jw);
 					const uint32_t hi = jw ? Ll[jw - 1u] : pred;
@@ -528,7 +544,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 					o.w = bswap32(__builtin_amdgcn_alignbit(wv.z, wv.w, r));
 					__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
 				}
-				const uint32_t rr = (tid - nquad) & 255u;
+				const uint32_t rr = (tid - nquad) & (ND - 1u);
 				if (rr < (nfull & 3u)) {
 					const uint32_t jw = 4u * nquad + rr;
 					const uint32_t hi = jw ? Ll[jw - 1u] : pred;
@@ -575,7 +591,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 			// clear what the previous acquisition used (words 0 .. (A+31)/32 - 1,
 			// and the one after for the flush); it packs acquisition acq + 1
 			const uint32_t nw = (A_prev + 63u) >> 5;
-			for (uint32_t i = tid; i < nw; i += 320u)
+			for (uint32_t i = tid; i < nw; i += NT)
 				imgp[i] = 0u;
 			// (visible to the next packing: after the next step's B1)
 		}
@@ -972,14 +988,27 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 template <int W, int PRE_P, int ENC_P, bool RICE_P>
 static bool walk_launch_s(const WArgs &k, uint32_t enc_s, bool rice_s, size_t lds, hipStream_t s)
 {
-	const dim3 grid(k.num_ctx * k.spf), blk(320);
-	if (enc_s == ENC_ZERO && rice_s)
-		hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true>), grid, blk, lds, s, k);
-	else if (enc_s == ENC_MULTI && rice_s)
-		hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true>), grid, blk, lds, s, k);
-	else
+	const dim3 grid(k.num_ctx * k.spf);
+	const bool two = k.spf * walk_seg_samples(true) == k.n && k.spf * walk_seg_samples(false) != k.n;
+	if (enc_s == ENC_ZERO && rice_s) {
+		if (two)
+			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 2>), grid, dim3(192), lds, s, k);
+		else
+			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 4>), grid, dim3(320), lds, s, k);
+	} else if (enc_s == ENC_MULTI && rice_s) {
+		if (two)
+			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 2>), grid, dim3(192), lds, s, k);
+		else
+			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 4>), grid, dim3(320), lds, s, k);
+	} else {
 		return false;
+	}
 	return true;
+}
+
+uint32_t walk_seg_samples(bool two_data_waves)
+{
+	return (two_data_waves ? 128u : 256u) * EPT;
 }
 
 template <int W, int PRE_P>

@@ -1454,6 +1454,12 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 
 // ---- MODEL streams in one launch (enc_walk.hip) ----------------------------
 
+// segment-walk workgroups below which the walk takes two data waves
+// (2048-sample segments): 0 = never; 1024 (twice the workgroups on cfg5s8)
+// measured slower, 155 against 96 us
+#ifndef AIRS_WALK_DW2_BELOW
+#define AIRS_WALK_DW2_BELOW 0u
+#endif
 // contexts from which a batch of walk_ctx_samples()-sample frames takes the
 // context walk (one workgroup per context) instead of the segment walk
 #ifndef AIRS_WALK_CTX_MIN
@@ -1497,7 +1503,10 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 {
 	if (!e || !airs_dev_walk_supported(w))
 		return ERRV(E_PARAMS_INVALID);
-	const uint32_t spf = w->n / AIRS_SEG;
+	// the segment walk takes two data waves (2048-sample segments) when four
+	// would leave fewer than four workgroups per CU (AIRS_WALK_DW2_BELOW)
+	const bool two = (uint64_t)w->num_ctx * (w->n / AIRS_SEG) < AIRS_WALK_DW2_BELOW;
+	const uint32_t spf = w->n / walk_seg_samples(two);
 	const uint64_t total = (uint64_t)w->num_ctx * w->fpc;
 	uint32_t r = ensure_granules(e, (size_t)(total * spf));
 	if (r)

@@ -525,13 +525,14 @@ def main():
     arena = ("airs::arena_kernel<DIFF,%s,%s> (enc_arena.hip: the Rice/ZERO fast path, one LDS arena per 16 Ki-sample "
              "segment%s)" % ("STREAM" if wname == "cfg2s" else "frames", "CTL" if ctl else "-",
                              ", a control wave runs the look-back" if ctl else ""))
-    if os.environ.get("AIRS_ARENA", "1") == "0":
-        arena = "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL> (AIRS_ARENA=0)"
+    if os.environ.get("AIRS_ARENA", "0") in ("", "0"):  # the arena kernel is opt-in
+        arena = ("airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL> (enc_kernel.h: 16 Ki-sample segments, decoupled "
+                 "look-back)")
     kernels = {
         "cfg2": arena + ": one launch per step",
         "cfg2s": arena + ": one launch per step, one look-back chain of 4096 segments",
         "cfg3": ("airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO>" if os.environ.get("AIRS_ARENA_AUTO") == "0" or
-                 os.environ.get("AIRS_ARENA") == "0" else "airs::arena_kernel<DIFF,frames,-,AUTO>") +
+                 os.environ.get("AIRS_ARENA", "0") in ("", "0") else "airs::arena_kernel<DIFF,frames,-,AUTO>") +
                 " (the per-frame Rice k chosen in-kernel from a histogram of the samples in registers): one launch "
                 "per step",
         "cfg4": arena + ": one launch per step",

@@ -5,7 +5,11 @@ batch compared with the oracle's call loop (include/cmp_gpu.h): frames, sizes
 and context state, bit-exact.  Cases cover every k the kernel takes, both
 sample types, checksums, several contexts, and segments that do not fit the
 arena (incompressible data: the one-chunk-per-pass path) next to segments
-that do, inside one frame."""
+that do, inside one frame.
+
+The arena kernel is an experiment, off by default (measured slower than
+encode_kernel): every case here turns it on with AIRS_ARENA=1,
+which the library reads at each launch."""
 import random
 
 import numpy as np
@@ -17,6 +21,11 @@ from conftest import load_pkg
 pytestmark = pytest.mark.gpu
 api = load_pkg().cmpapi
 SEG = 16384  # samples per segment of the arena kernel (enc_arena.hip ASEGN)
+
+
+@pytest.fixture(autouse=True)
+def arena_on(monkeypatch):
+    monkeypatch.setenv("AIRS_ARENA", "1")
 
 
 @pytest.fixture(scope="module")

@@ -68,6 +68,7 @@ def _oracle(orc, orc_ext, kind, pre, frames):
                 primary_encoder_param=1 << k)
         assert not api.is_error(orc.initialise(ctx, prm))
         cap = orc.compress_bound(2 * n)
+        cap = cap if not api.is_error(cap) else 6 * n + 64  # past the 24-bit size field's worst case
         dst = api.aligned_empty(cap)
         r = orc.compress(kind, ctx, dst, cap, x)
         assert not api.is_error(r), api.error_name(r)
@@ -135,6 +136,17 @@ def test_autorice_vs_oracle(prod, eng, orc, orc_ext, kind, pre, n):
     bad = [f for f in range(nf) if _mask(got[f]) != _mask(want[f])]
     assert not bad, (f"frames {bad[:8]} differ; g gpu/oracle "
                      f"{[(api.parse_header(got[f])['encoder_param'], api.parse_header(want[f])['encoder_param']) for f in bad[:4]]}")
+
+
+ARENA_CASES = [("u16", 1, SEG16), ("i16", 0, 4 * SEG16), ("u16", 0, AUTO_MAX_SPF * SEG16), ("u16", 1, 4 << 20)]
+
+
+@pytest.mark.parametrize("kind,pre,n", ARENA_CASES)
+def test_autorice_arena_vs_oracle(prod, eng, orc, orc_ext, monkeypatch, kind, pre, n):
+    """The same cases through the arena kernel's fused selection (an
+    experiment, off by default: AIRS_ARENA=1, read at each launch)."""
+    monkeypatch.setenv("AIRS_ARENA", "1")
+    test_autorice_vs_oracle(prod, eng, orc, orc_ext, kind, pre, n)
 
 
 def test_autorice_k_range(prod, eng, orc, orc_ext):

@@ -19,23 +19,24 @@ LIB = os.path.join(PKG_DIR, "lib", "libairscmp.so")
 
 # symbol: (max VGPRs, max SGPR spills to VGPR lanes); VGPR spills must be 0
 BUDGETS = {
-    # cfg2 / cfg4: the arena kernel, DIFF and NONE, frames (5 waves per SIMD);
-    # and its control-wave form (AIRS_ARENA_CTL)
+    # the arena kernel (an experiment, AIRS_ARENA=1), DIFF and NONE, frames (5
+    # waves per SIMD); and its control-wave form (AIRS_ARENA_CTL)
     "_ZN4airs12arena_kernelILi1ELb0ELb0ELb0EEEvNS_5KArgsE": (96, 17),
     "_ZN4airs12arena_kernelILi0ELb0ELb0ELb0EEEvNS_5KArgsE": (96, 17),
     "_ZN4airs12arena_kernelILi1ELb0ELb1ELb0EEEvNS_5KArgsE": (96, 28),
-    # cfg3: the arena kernel with the fused per-frame Rice selection
+    # the arena kernel with the fused per-frame Rice selection
     "_ZN4airs12arena_kernelILi1ELb0ELb0ELb1EEEvNS_5KArgsE": (96, 0),
-    # encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>: AIRS_ARENA=0 and the other shapes
+    # cfg2 / cfg4: encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb0EEEvNS_5KArgsE": (128, 13),
-    # encode_kernel's fused per-frame Rice selection (AIRS_ARENA_AUTO=0, partial segments)
+    # cfg3: encode_kernel's fused per-frame Rice selection
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb1ELb0EEEvNS_5KArgsE": (128, 0),
     # cfg2s: payload-only stream
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb1EEEvNS_5KArgsE": (128, 0),
     # cfg5 / cfg5fb: the context walk (1024-thread workgroups: <= 128 VGPRs)
     "_ZN4airs15walk_ctx_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi4EEEvNS_5WArgsE": (128, 34),
-    # cfg5s8: the segment walk (320-thread workgroups)
-    "_ZN4airs11walk_kernelILi4ELi1ELi1ELb1ELi2ELb1EEEvNS_5WArgsE": (96, 38),
+    # the segment walk, four data waves (cfg5s8) and two (AIRS_WALK_DW2_BELOW)
+    "_ZN4airs11walk_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi4EEEvNS_5WArgsE": (96, 40),
+    "_ZN4airs11walk_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi2EEEvNS_5WArgsE": (96, 36),
 }
 
 
