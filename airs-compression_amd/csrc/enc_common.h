@@ -488,7 +488,7 @@ bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint
 uint32_t walk_ctx_samples();
 // samples per segment of the segment walk (walk_kernel): 4096 with four data
 // waves, 2048 with two (batches of few contexts); k.spf = n / that
-uint32_t walk_seg_samples(bool two_data_waves);
+uint32_t walk_seg_samples(bool half);
 // the arena kernel (enc_arena.hip): 16-bit NONE/DIFF GOLOMB_ZERO g = 2^k <=
 // 2048, no model, whole segments; k.img_words = arena_words()
 bool arena_encode(const KArgs &k, uint32_t pre, bool stream, uint32_t grid, hipStream_t s);

@@ -136,26 +136,26 @@ __device__ __forceinline__ void store_b32_nc(uint32_t v, uint32_t byte_off, u32x
 
 // one pass's residual-independent coding: table offsets (8 idx per sample,
 // 16-bit halves of oq[]), lengths total of the lane; returns the lane's bits
-template <int ENC, bool RICE>
-__device__ __forceinline__ uint32_t walk_lengths(const uint32_t (&mp)[EPT / 2], uint32_t (&oq)[EPT / 2],
-						 const Coder &cd, bool fast, const char *tab)
+template <int ENC, bool RICE, int NP>
+__device__ __forceinline__ uint32_t walk_lengths(const uint32_t (&mp)[NP], uint32_t (&oq)[NP], const Coder &cd,
+						 bool fast, const char *tab)
 {
 	uint32_t t = 0u;
 	if (ENC == ENC_ZERO && RICE && fast) {
 		u16x2 acc = (u16x2)(0);
 #pragma unroll
-		for (uint32_t j = 0; j < EPT / 2; j++) {
+		for (uint32_t j = 0; j < NP; j++) {
 			const u16x2 v = __builtin_elementwise_add_sat(pk(mp[j]), (u16x2)(1));
 			const u16x2 q = v >> (u16x2)((unsigned short)cd.k);
 			acc += __builtin_elementwise_min(q, (u16x2)(16));
 			oq[j] = unpk(__builtin_elementwise_min(q, (u16x2)(17)) << (u16x2)(3));
 		}
-		return EPT * (cd.k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
+		return 2u * NP * (cd.k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
 	}
 	if (ENC == ENC_MULTI && RICE) {
 		const uint32_t om1 = cd.outlier - 1u;
 #pragma unroll
-		for (uint32_t j = 0; j < EPT / 2; j++) {
+		for (uint32_t j = 0; j < NP; j++) {
 			uint32_t o2 = 0u;
 #pragma unroll
 			for (uint32_t h = 0; h < 2u; h++) {
@@ -171,45 +171,46 @@ __device__ __forceinline__ uint32_t walk_lengths(const uint32_t (&mp)[EPT / 2], 
 		return t;
 	}
 #pragma unroll
-	for (uint32_t j = 0; j < EPT; j++)
+	for (uint32_t j = 0; j < 2u * NP; j++)
 		t += len_from_m<ENC, RICE>(half16(mp[j >> 1], j & 1u), cd);
 	return t;
 }
 
-// pack the lane's 16 codewords from bit `excl` of the image
-template <int ENC, bool RICE>
-__device__ __forceinline__ void walk_pack(uint32_t *img, uint32_t excl, const uint32_t (&mp)[EPT / 2],
-					  const uint32_t (&oq)[EPT / 2], const Coder &cd, bool fast, const char *tab)
+// pack the lane's 2 NP codewords from bit `excl` of the image
+template <int ENC, bool RICE, int NP>
+__device__ __forceinline__ void walk_pack(uint32_t *img, uint32_t excl, const uint32_t (&mp)[NP],
+					  const uint32_t (&oq)[NP], const Coder &cd, bool fast, const char *tab)
 {
+	static_assert(NP % 4 == 0, "batches of 8 samples");
 	Packer pk1;
 	pk1.init(img, excl);
 	if (ENC == ENC_ZERO && RICE && fast) {
 #pragma unroll
-		for (uint32_t hb = 0; hb < 2; hb++) { // two batches of 8 lookups (pairs of codewords per put)
-			uint2 te[EPT / 2];
+		for (uint32_t hb = 0; hb < NP / 4u; hb++) { // batches of 8 lookups (pairs of codewords per put)
+			uint2 te[8];
 #pragma unroll
-			for (uint32_t jj = 0; jj < EPT / 4; jj++) {
-				const uint32_t j = hb * (EPT / 4) + jj;
+			for (uint32_t jj = 0; jj < 4u; jj++) {
+				const uint32_t j = hb * 4u + jj;
 #pragma unroll
 				for (uint32_t h = 0; h < 2; h++)
 					te[2 * jj + h] = *reinterpret_cast<const uint2 *>(tab + half16(oq[j], h));
 			}
 			uint32_t mxl = 0u;
 #pragma unroll
-			for (uint32_t i = 0; i < EPT / 2; i += 2)
+			for (uint32_t i = 0; i < 8u; i += 2)
 				mxl = max(mxl, te[i].y + te[i + 1].y);
 			if (__ballot(mxl > 32u) == 0ull) {
 #pragma unroll
-				for (uint32_t i = 0; i < EPT / 2; i += 2) {
-					const uint32_t j = hb * (EPT / 2) + i;
+				for (uint32_t i = 0; i < 8u; i += 2) {
+					const uint32_t j = hb * 8u + i;
 					const uint32_t cwa = (mp[j >> 1] & 0xFFFFu) + te[i].x;
 					const uint32_t cwb = (mp[j >> 1] >> 16) + te[i + 1].x;
 					pk1.put((cwa << te[i + 1].y) | cwb, te[i].y + te[i + 1].y);
 				}
 			} else {
 #pragma unroll
-				for (uint32_t i = 0; i < EPT / 2; i += 2) {
-					const uint32_t j = hb * (EPT / 2) + i;
+				for (uint32_t i = 0; i < 8u; i += 2) {
+					const uint32_t j = hb * 8u + i;
 					pk1.put((mp[j >> 1] & 0xFFFFu) + te[i].x, te[i].y);
 					pk1.put((mp[j >> 1] >> 16) + te[i + 1].x, te[i + 1].y);
 				}
@@ -217,7 +218,7 @@ __device__ __forceinline__ void walk_pack(uint32_t *img, uint32_t excl, const ui
 		}
 	} else if (ENC == ENC_MULTI && RICE) {
 #pragma unroll
-		for (uint32_t j = 0; j < EPT; j++) {
+		for (uint32_t j = 0; j < 2u * NP; j++) {
 			const uint32_t m = half16(mp[j >> 1], j & 1u);
 			const uint32_t off = half16(oq[j >> 1], j & 1u);
 			const uint2 e = *reinterpret_cast<const uint2 *>(tab + off);
@@ -231,7 +232,7 @@ __device__ __forceinline__ void walk_pack(uint32_t *img, uint32_t excl, const ui
 		}
 	} else {
 #pragma unroll
-		for (uint32_t j = 0; j < EPT; j++) {
+		for (uint32_t j = 0; j < 2u * NP; j++) {
 			uint32_t c1, l1, c2, l2;
 			code_from_m<ENC, RICE>(half16(mp[j >> 1], j & 1u), cd, c1, l1, c2, l2);
 			pk1.put(c1, l1);
@@ -248,17 +249,20 @@ __device__ __forceinline__ uint32_t hdr_bits(int pre, int enc)
 	return (pre == PRE_NONE && enc == ENC_RAW) ? 128u : 176u;
 }
 
-// DW data waves (2 or 4) and one control wave: a segment is DW * 1024
-// samples.  Two data waves double the workgroups of a batch, for batches of
-// few contexts (configs[4]'s 32 streams per GPU at N = 8: 1024 workgroups
-// instead of 512, four per CU instead of two).
-template <int W, int PRE_P, int ENC_P, bool RICE_P, int ENC_S, bool RICE_S, int DW>
-__global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
+// Four data waves of E samples per lane (16 or 8) and one control wave: a
+// segment is 256 E samples.  E = 8 doubles the workgroups (and the waves) of
+// a batch, for batches of few contexts (configs[4]'s 32 streams per GPU at
+// N = 8: 1024 workgroups instead of 512, 4 data waves per SIMD instead of 2):
+// a step is latency-bound per wave (LDS lookups and puts in the packing), so
+// twice the waves with half the samples each shorten it.
+template <int W, int PRE_P, int ENC_P, bool RICE_P, int ENC_S, bool RICE_S, int E>
+__global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 {
-	static_assert(DW == 2 || DW == 4, "two or four data waves");
-	constexpr uint32_t RW = EPT * W / 16u; // uint4 per lane
+	static_assert(E == 16 || E == 8, "16 or 8 samples per lane");
+	constexpr uint32_t DW = 4u;
+	constexpr uint32_t RW = E * W / 16u; // uint4 per lane
 	constexpr uint32_t NT = 64u * (DW + 1u), ND = 64u * DW; // threads, data threads
-	constexpr uint32_t SEGW = ND * EPT;                      // samples per segment
+	constexpr uint32_t SEGW = ND * E;                        // samples per segment
 	extern __shared__ __attribute__((aligned(16))) uint32_t L_img[];
 	__shared__ uint32_t s_wsum[DW];
 	__shared__ uint32_t s_ctl[4];
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 	const uint32_t c = lb / a.spf, j = lb - c * a.spf;
 	const bool is_first = j == 0u, is_last = j + 1u == a.spf;
 	const uint32_t n = a.n;
-	const uint32_t first = j * SEGW + (data ? tid : 0u) * EPT; // lane's first sample
+	const uint32_t first = j * SEGW + (data ? tid : 0u) * E; // lane's first sample
 	uint16_t *mbase = reinterpret_cast<uint16_t *>(a.model_ptrs ? (uint8_t *)(uintptr_t)a.model_ptrs[c]
 								    : a.model + (uint64_t)c * a.model_stride);
 	// two images (a.img_words each, after a 4-word pad): acquisition a packs
@@ -306,14 +310,14 @@ __global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 	// differences and do not change
 	const uint32_t flip = a.is_unsigned ? 0u : 0x80008000u;
 	// the model of this lane's 16 samples, packed pairs
-	uint32_t mdl[EPT / 2];
+	uint32_t mdl[E / 2];
 #pragma unroll
-	for (uint32_t q = 0; q < EPT / 2; q++)
+	for (uint32_t q = 0; q < E / 2; q++)
 		mdl[q] = 0u;
 	if (data && seq0 != 0u && seq0 <= a.iters) { // the first frame is a secondary pass
 		const uint4 *mp4 = reinterpret_cast<const uint4 *>(mbase + first);
 #pragma unroll
-		for (uint32_t q = 0; q < EPT / 8; q++) {
+		for (uint32_t q = 0; q < E / 8; q++) {
 			const uint4 v = mp4[q];
 			mdl[4 * q] = v.x ^ flip;
 			mdl[4 * q + 1] = v.y ^ flip;
@@ -346,8 +350,9 @@ __global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 	bool prim_prev = false;
 	// Step `acq` codes acquisition acq (acq < fpc) and stores acquisition
 	// acq - 1 (acq > 0).  The look-back of acquisition acq - 1 runs in step acq:
-	// every segment published its aggregate for it one step earlier, so it is
-	// one granule round trip, overlapped with this step's packing, and never
+	// every segment published its aggregate and tail for it one step earlier,
+	// so it is one granule round trip (look-back window and tail together),
+	// issued before B1 and overlapped with phase 1 and the packing, and never
 	// waits on a chain of predecessors.
 	for (uint32_t acq = 0; acq <= a.fpc; acq++) {
 		const bool have = acq < a.fpc, prev = acq > 0u;
@@ -359,11 +364,11 @@ __global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 		const uint32_t HB = prim ? hdr_bits(PRE_P, ENC_P) : hdr_bits(PRE_MODEL, ENC_S);
 		uint32_t *const img = (acq & 1u) ? img1 : img0;
 		uint32_t *const imgp = (acq & 1u) ? img0 : img1;
-		uint32_t mp[EPT / 2], oq[EPT / 2];
+		uint32_t mp[E / 2], oq[E / 2];
 		uint32_t T = 0u, excl = 0u;
 		if (have && data) {
 			// ---- phase 1: samples, residuals, model update, lengths ----------
-			uint32_t w[EPT / 2];
+			uint32_t w[E / 2];
 			if (W == 2) {
 #pragma unroll
 				for (uint32_t q = 0; q < RW; q++) {
@@ -387,12 +392,12 @@ __global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 			if (prim) {
 				uint32_t wprev = 0u;
 				if (PRE_P == PRE_DIFF) {
-					wprev = __shfl_up(w[EPT / 2 - 1], 1, 64);
+					wprev = __shfl_up(w[E / 2 - 1], 1, 64);
 					if (lane == 0u)
 						wprev = (prevs << 16) ^ flip;
 				}
 #pragma unroll
-				for (uint32_t q = 0; q < EPT / 2; q++) {
+				for (uint32_t q = 0; q < E / 2; q++) {
 					uint32_t u = w[q] ^ flip; // NONE: the sample itself
 					if (PRE_P == PRE_DIFF)
 						u = unpk(pk(w[q]) - pk(__builtin_amdgcn_alignbit(w[q], q ? w[q - 1] : wprev, 16)));
@@ -403,7 +408,7 @@ __global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 			} else {
 				const int32_t r1 = 16 - (int32_t)a.model_rate;
 #pragma unroll
-				for (uint32_t q = 0; q < EPT / 2; q++) {
+				for (uint32_t q = 0; q < E / 2; q++) {
 					const uint32_t u = unpk(pk(w[q]) - pk(mdl[q])); // preprocess.c:406-411
 					mp[q] = ENC_S == ENC_RAW ? u : zigzag_pk(u);
 					mdl[q] = model_update_zx(w[q], mdl[q], r1); // cmp.c:132-142
@@ -411,12 +416,24 @@ __global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 				T = walk_lengths<ENC_S, RICE_S>(mp, oq, cs, fast_s, tab_s);
 			}
 #pragma unroll
-			for (uint32_t q = 0; q < EPT / 2; q++)
+			for (uint32_t q = 0; q < E / 2; q++)
 				asm volatile("" : "+v"(mp[q]), "+v"(oq[q]));
 			const uint32_t inc = wave_incl_scan(T);
 			if (lane == 63u)
 				s_wsum[wid] = inc;
 			excl = inc - T;
+		}
+		// control wave: the first look-back round of acquisition acq - 1 and its
+		// predecessor tail, issued together now and evaluated after B1 (one round
+		// trip, overlapped with phase 1; the segments before it published both
+		// during the previous step)
+		uint64_t gv0 = 0ull, tv0 = 0ull;
+		if (!data && prev && !is_first) {
+			const uint64_t gseg = (uint64_t)(f - 1u) * a.spf + j;
+			const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane;
+			if (lane == 0u)
+				tv0 = gran_load(&a.tail[gseg - 1u]);
+			gv0 = idx >= (int64_t)(gseg - j) ? gran_load(&a.agg[idx]) : 0ull;
 		}
 		lds_barrier(); // B1: wave totals
 		uint32_t Asum = 0u, wpre = 0u;
@@ -464,10 +481,10 @@ __global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 					const uint64_t first_seg = gseg - j;
 					uint32_t sum = 0u, spins = 0u;
 					int64_t jj = (int64_t)gseg - 1;
+					uint64_t gv = gv0;
 					for (;;) {
 						const int64_t idx = jj - (int64_t)lane;
 						const bool inr = idx >= (int64_t)first_seg;
-						const uint64_t gv = inr ? gran_load(&a.agg[idx]) : 0ull;
 						const uint32_t tag = (uint32_t)(gv >> 32);
 						const bool valid = inr && (tag >> 1) == a.epoch;
 						const bool incl = valid && (tag & 1u);
@@ -482,23 +499,24 @@ __global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 								break;
 							}
 							__builtin_amdgcn_s_sleep(1);
+							gv = inr ? gran_load(&a.agg[idx]) : 0ull;
 							continue;
 						}
 						sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv : 0u);
 						if (incl_m)
 							break;
 						jj -= 64;
+						gv = jj - (int64_t)lane >= (int64_t)first_seg ? gran_load(&a.agg[jj - (int64_t)lane]) : 0ull;
 					}
 					P = sum;
 					if (lane == 0u)
 						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (P + A_prev));
 					wstamp(a, acq - 1u, 5u);
 					// the predecessor's last 32 bits (published after its packing)
-					uint64_t tv = 0ull;
+					uint64_t tv = tv0;
 					if (lane == 0u) {
 						uint32_t sp = 0u;
-						for (tv = gran_load(&a.tail[gseg - 1u]); (uint32_t)(tv >> 32) != a.epoch;
-						     tv = gran_load(&a.tail[gseg - 1u])) {
+						for (; (uint32_t)(tv >> 32) != a.epoch; tv = gran_load(&a.tail[gseg - 1u])) {
 							if (++sp > AIRS_SPIN_LIMIT) {
 								atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
 								break;
@@ -604,7 +622,7 @@ __global__ __launch_bounds__(64 * (DW + 1)) void walk_kernel(WArgs a)
 	if (data) {
 		uint4 *mo = reinterpret_cast<uint4 *>(mbase + first);
 #pragma unroll
-		for (uint32_t q = 0; q < EPT / 8; q++)
+		for (uint32_t q = 0; q < E / 8; q++)
 			mo[q] = make_uint4(mdl[4 * q] ^ flip, mdl[4 * q + 1] ^ flip, mdl[4 * q + 2] ^ flip, mdl[4 * q + 3] ^ flip);
 	}
 }
@@ -989,26 +1007,27 @@ template <int W, int PRE_P, int ENC_P, bool RICE_P>
 static bool walk_launch_s(const WArgs &k, uint32_t enc_s, bool rice_s, size_t lds, hipStream_t s)
 {
 	const dim3 grid(k.num_ctx * k.spf);
-	const bool two = k.spf * walk_seg_samples(true) == k.n && k.spf * walk_seg_samples(false) != k.n;
+	const bool half = k.spf * walk_seg_samples(true) == k.n && k.spf * walk_seg_samples(false) != k.n;
 	if (enc_s == ENC_ZERO && rice_s) {
-		if (two)
-			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 2>), grid, dim3(192), lds, s, k);
+		if (half)
+			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 8>), grid, dim3(320), lds, s, k);
 		else
-			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 4>), grid, dim3(320), lds, s, k);
+			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 16>), grid, dim3(320), lds, s, k);
 	} else if (enc_s == ENC_MULTI && rice_s) {
-		if (two)
-			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 2>), grid, dim3(192), lds, s, k);
+		if (half)
+			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 8>), grid, dim3(320), lds, s, k);
 		else
-			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 4>), grid, dim3(320), lds, s, k);
+			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 16>), grid, dim3(320), lds, s, k);
 	} else {
 		return false;
 	}
 	return true;
 }
 
-uint32_t walk_seg_samples(bool two_data_waves)
+// samples per segment of the segment walk: 256 lanes of 16 samples, or of 8
+uint32_t walk_seg_samples(bool half)
 {
-	return (two_data_waves ? 128u : 256u) * EPT;
+	return half ? 2048u : 4096u;
 }
 
 template <int W, int PRE_P>

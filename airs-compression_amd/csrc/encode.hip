@@ -1454,11 +1454,11 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 
 // ---- MODEL streams in one launch (enc_walk.hip) ----------------------------
 
-// segment-walk workgroups below which the walk takes two data waves
-// (2048-sample segments): 0 = never; 1024 (twice the workgroups on cfg5s8)
-// measured slower, 155 against 96 us
-#ifndef AIRS_WALK_DW2_BELOW
-#define AIRS_WALK_DW2_BELOW 0u
+// segment-walk workgroups (of 4096 samples) below which the walk takes
+// 2048-sample segments, 8 samples per lane: twice the workgroups and waves
+// (cfg5s8: 512 -> 1024 workgroups, 2 -> 4 data waves per SIMD)
+#ifndef AIRS_WALK_HALF_BELOW
+#define AIRS_WALK_HALF_BELOW 1024u
 #endif
 // contexts from which a batch of walk_ctx_samples()-sample frames takes the
 // context walk (one workgroup per context) instead of the segment walk
@@ -1503,10 +1503,12 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 {
 	if (!e || !airs_dev_walk_supported(w))
 		return ERRV(E_PARAMS_INVALID);
-	// the segment walk takes two data waves (2048-sample segments) when four
-	// would leave fewer than four workgroups per CU (AIRS_WALK_DW2_BELOW)
-	const bool two = (uint64_t)w->num_ctx * (w->n / AIRS_SEG) < AIRS_WALK_DW2_BELOW;
-	const uint32_t spf = w->n / walk_seg_samples(two);
+	// the segment walk takes 2048-sample segments when 4096-sample ones would
+	// leave fewer than four workgroups per CU (AIRS_WALK_HALF_BELOW)
+	bool half = (uint64_t)w->num_ctx * (w->n / AIRS_SEG) < AIRS_WALK_HALF_BELOW;
+	if (const char *sg = getenv("AIRS_WALK_SEG")) // tests and A/B: 2048 or 4096 forces the segment size
+		half = atoi(sg) == 2048 ? true : atoi(sg) == 4096 ? false : half;
+	const uint32_t spf = w->n / walk_seg_samples(half);
 	const uint64_t total = (uint64_t)w->num_ctx * w->fpc;
 	uint32_t r = ensure_granules(e, (size_t)(total * spf));
 	if (r)
@@ -1548,9 +1550,14 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 	k.raw_size = w->raw_size;
 	k.draws = w->draws;
 	k.seq_out = w->seq_out;
-	// one image for the longer-coded of the two passes (plus a flush word)
-	const uint32_t iw_p = image_words(w->enc_p, w->g_p), iw_s = image_words(w->enc_s, w->g_s);
-	k.img_words = (iw_p > iw_s ? iw_p : iw_s) + 4u;
+	// one image for a segment of the longer-coded of the two passes at its
+	// longest codeword, plus flush words (cfg5's MULTI g = 8: 34 bits, 17 KiB;
+	// sized for 48 bits, two-data-wave workgroups did not all fit the CUs)
+	{
+		const uint32_t mbp = code_max_bits(w->enc_p, w->g_p, w->outl_p);
+		const uint32_t mbs = code_max_bits(w->enc_s, w->g_s, w->outl_s);
+		k.img_words = ((walk_seg_samples(half) * (mbp > mbs ? mbp : mbs) / 32u + 8u) + 3u) & ~3u;
+	}
 	k.epoch = next_epoch(e);
 	// one context per workgroup when the frames have its size, there are
 	// enough contexts to fill the CUs, and two images fit the LDS
@@ -1582,7 +1589,6 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 		k.dbgts = e->dbgts;
 	}
 #endif
-	// images: the longer-coded pass's 4096 samples, plus the flush word
 	k.ticket_base = e->walk_ticket_base;
 	if (!walk_encode(k, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream))
 		return ERRV(E_PARAMS_INVALID);

@@ -538,9 +538,9 @@ def main():
         "cfg4": arena + ": one launch per step",
         "cfg5": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> (enc_walk.hip): ONE launch per step, one "
                 "1024-thread workgroup per stream walks its 16 acquisitions, the model in registers",
-        "cfg5s8": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice> (enc_walk.hip, the segment walk): ONE launch per "
-                  "step, a 320-thread workgroup per (stream, 4096-sample segment) walks the 16 acquisitions, each "
-                  "acquisition's look-back resolved one step later",
+        "cfg5s8": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,8> (enc_walk.hip, the segment walk): ONE launch "
+                  "per step, a 320-thread workgroup per (stream, 2048-sample segment, 8 samples per lane) walks the "
+                  "16 acquisitions, each acquisition's look-back resolved one step later",
         "cfg5fb": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> with the uncompressed fallback resolved on "
                   "the chip: ONE launch per step, then one read-back of the draw counts and the identifier patch "
                   "(patch_ids_kernel)",

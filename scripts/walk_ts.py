@@ -33,7 +33,8 @@ for i in range(3):
     assert eng.synchronize() == 0
 fpc = wl["fpc"]
 ts = np.fromfile(raw, dtype=np.uint64)
-nb = wl["nctx"] * (wl["n"] // 4096)
+SEGN = int(os.environ.get("AIRS_TS_SEG", "4096"))  # samples per segment (2048: two data waves)
+nb = wl["nctx"] * (wl["n"] // SEGN)
 ts = ts[:nb * fpc * 8].reshape(nb, fpc, 8).astype(np.int64)
 os.remove(raw)
 t0 = ts[:, 0, 0].min()
@@ -53,7 +54,7 @@ def pct(x, q):
 rel = ts[:, :, :7] - t0
 start = rel[:, 0, 0]
 end = rel[:, -1, 4]
-spf = wl["n"] // 4096
+spf = wl["n"] // SEGN
 j = np.arange(nb) % spf
 notfirst = j != 0
 res = dict(

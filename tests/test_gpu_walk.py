@@ -165,8 +165,12 @@ def make_case(trial):
     return params, kind, n, nctx, calls, cap
 
 
-@pytest.mark.parametrize("block", range(6))
-def test_walk_vs_call_loop(prod, eng, orc, block):
+@pytest.mark.parametrize("block,seg", [(b, None) for b in range(6)] + [(b, "4096") for b in range(3)])
+def test_walk_vs_call_loop(prod, eng, orc, monkeypatch, block, seg):
+    """seg: these few-context batches take 2048-sample segments (8 samples per
+    lane); AIRS_WALK_SEG=4096 forces the 16-sample form on the same trials."""
+    if seg:
+        monkeypatch.setenv("AIRS_WALK_SEG", seg)
     bad = []
     for trial in range(block * 12, block * 12 + 12):
         params, kind, n, nctx, calls, cap = make_case(trial)
@@ -234,14 +238,18 @@ CTX_CASES = [  # (kind, pre_p, enc_p, g_p, o_p, enc_s, g_s, o_s, iters, rate, ch
 ]
 
 
-@pytest.mark.parametrize("case,nctx", [(c, 128) for c in range(len(CTX_CASES))] + [(0, 32), (4, 32)])
-def test_walk_ctx_vs_call_loop(prod, eng, orc, case, nctx):
+@pytest.mark.parametrize("case,nctx,seg", [(c, 128, None) for c in range(len(CTX_CASES))] +
+                         [(0, 32, None), (4, 32, None), (0, 32, "4096"), (2, 32, None)])
+def test_walk_ctx_vs_call_loop(prod, eng, orc, monkeypatch, case, nctx, seg):
     """Batches of >= 128 contexts of 64 Ki-sample frames take the context walk
     (one workgroup per context, walk_ctx_kernel); 32 contexts (configs[4]'s
     per-GPU share at N = 8) take the segment walk (walk_kernel, each
-    acquisition's look-back one step late).  Frames, sizes, context states and
-    work buffers equal the call loop; two calls in a row, so the second starts
-    mid-sequence with the model read back from the work buffers."""
+    acquisition's look-back one step late; 2048-sample segments, or 4096 with
+    AIRS_WALK_SEG).  Frames, sizes, context states and work buffers equal the
+    call loop; two calls in a row, so the second starts mid-sequence with the
+    model read back from the work buffers."""
+    if seg:
+        monkeypatch.setenv("AIRS_WALK_SEG", seg)
     kind, pre, ep, gp, op, es, gs, osx, iters, rate, ck = CTX_CASES[case]
     rng = np.random.default_rng(500 + case + nctx)
     n = 65536
@@ -317,13 +325,16 @@ def test_whole_unit_frames_vs_call_loop(prod, eng, orc, case):
     assert sw == sg
 
 
-def test_segment_walk_more_workgroups_than_resident(prod, eng, orc):
+@pytest.mark.parametrize("seg", [None, "2048"])
+def test_segment_walk_more_workgroups_than_resident(prod, eng, orc, monkeypatch, seg):
     """a segment walk whose grid exceeds what the GPU holds at once
     (1100 contexts x one 4096-sample segment, 320-thread workgroups with two
-    images each, fewer than 1100 resident) and a long walk (12 acquisitions):
-    the workgroups take logical indices from a ticket, so a look-back only
-    waits on a running workgroup; no give-up, frames and state equal the call
-    loop."""
+    images each: at most 1024 resident; or x two 2048-sample segments, 2200
+    workgroups, at most 1280 resident) and a long walk (12 acquisitions): the
+    workgroups take logical indices from a ticket, so a look-back only waits
+    on a running workgroup; no give-up, frames and state equal the call loop."""
+    if seg:
+        monkeypatch.setenv("AIRS_WALK_SEG", seg)
     rng = np.random.default_rng(31)
     kind, n, nctx, fpc = "u16", 4096, 1100, 12
     p = P(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16, secondary_iterations=15,
