@@ -46,6 +46,11 @@ namespace airs {
 
 // rows of the code tables in LDS (one table per pass)
 #define WTAB 48u
+// LDS images of the segment walk (2: a third barrier per step clears the
+// image of the acquisition just stored; 3: no third barrier)
+#ifndef AIRS_WALK_NIMG
+#define AIRS_WALK_NIMG 3u
+#endif
 
 // table entry idx of a pass: {T, len}; see the header comment
 template <int ENC>
@@ -285,10 +290,12 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 	const uint32_t first = j * SEGW + (data ? tid : 0u) * E; // lane's first sample
 	uint16_t *mbase = reinterpret_cast<uint16_t *>(a.model_ptrs ? (uint8_t *)(uintptr_t)a.model_ptrs[c]
 								    : a.model + (uint64_t)c * a.model_stride);
-	// two images (a.img_words each, after a 4-word pad): acquisition a packs
-	// into image a % 2 and is stored in the next step, once its frame offset
-	// is known
-	uint32_t *const img0 = L_img + 4u, *const img1 = L_img + 8u + a.img_words;
+	// NIMG images (a.img_words each, after a 4-word pad): acquisition a packs
+	// into image a % NIMG and is stored in the next step, once its frame
+	// offset is known.  With three, the image acquisition a + 1 packs into was
+	// stored two steps earlier, so it is cleared without a third barrier
+	constexpr uint32_t NIMG = AIRS_WALK_NIMG;
+	auto img_at = [&](uint32_t q) { return L_img + 4u + (q % NIMG) * (a.img_words + 4u); };
 
 	const Coder cp = make_coder<ENC_P>(ENC_P == ENC_RAW ? 1u : a.g_p, a.outl_p);
 	const Coder cs = make_coder<ENC_S>(ENC_S == ENC_RAW ? 1u : a.g_s, a.outl_s);
@@ -300,7 +307,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		if (fast_s)
 			s_tab[1][tid] = walk_table_entry<ENC_S>(tid, cs);
 	}
-	for (uint32_t i = tid; i < 2u * a.img_words + 8u; i += NT)
+	for (uint32_t i = tid; i < NIMG * (a.img_words + 4u) + 4u; i += NT)
 		L_img[i] = 0u;
 
 	const uint32_t seq0 = a.seq0s ? a.seq0s[c] : a.seq0;
@@ -328,15 +335,21 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 	// prefetch of acquisition 0
 	uint4 rn[RW];
 	uint32_t pn = 0u;
+	// unconditional loads, every data lane (the sample before the lane's first
+	// matters to lane 0 only; its low half is taken at the use): a load under
+	// a condition into registers that stay live makes the compiler wait for
+	// it, and for the prefetch issued with it, right after the issue
 	auto issue = [&](uint32_t acq) {
 		const uint8_t *fs = a.src + (uint64_t)(c * a.fpc + acq) * a.src_stride;
 		const uint4 *p = reinterpret_cast<const uint4 *>(fs + (size_t)first * W);
 #pragma unroll
 		for (uint32_t q = 0; q < RW; q++)
 			rn[q] = p[q];
-		if (PRE_P == PRE_DIFF && lane == 0u && first != 0u)
-			pn = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fs)[first - 1u]
-				    : reinterpret_cast<const uint32_t *>(fs)[first - 1u] & 0xFFFFu;
+		if (PRE_P == PRE_DIFF) {
+			const uint32_t ip = first ? first - 1u : 0u;
+			pn = W == 2 ? (uint32_t)reinterpret_cast<const uint16_t *>(fs)[ip]
+				    : reinterpret_cast<const uint32_t *>(fs)[ip];
+		}
 	};
 	if (data)
 		issue(0u);
@@ -346,7 +359,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 	const char *tab_s = reinterpret_cast<const char *>(s_tab[1]);
 	uint32_t sq = seq0;
 	// the previous acquisition (packed, waiting for its frame offset)
-	uint32_t A_prev = 0u, HB_prev = 0u, hseq_prev = 0u;
+	uint32_t A_prev = 0u, A_prev2 = 0u, HB_prev = 0u, hseq_prev = 0u;
 	bool prim_prev = false;
 	// Step `acq` codes acquisition acq (acq < fpc) and stores acquisition
 	// acq - 1 (acq > 0).  The look-back of acquisition acq - 1 runs in step acq:
@@ -362,8 +375,8 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		if (have)
 			sq = prim ? 1u : sq + 1u;
 		const uint32_t HB = prim ? hdr_bits(PRE_P, ENC_P) : hdr_bits(PRE_MODEL, ENC_S);
-		uint32_t *const img = (acq & 1u) ? img1 : img0;
-		uint32_t *const imgp = (acq & 1u) ? img0 : img1;
+		uint32_t *const img = img_at(acq);
+		uint32_t *const imgp = img_at(acq + NIMG - 1u);
 		uint32_t mp[E / 2], oq[E / 2];
 		uint32_t T = 0u, excl = 0u;
 		if (have && data) {
@@ -386,9 +399,8 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 			}
 			if (wid == 0u)
 				wstamp(a, acq, 0u);
-			const uint32_t prevs = pn;
-			if (acq + 1u < a.fpc)
-				issue(acq + 1u); // lands while this acquisition packs
+			const uint32_t prevs = first ? pn & 0xFFFFu : 0u;
+			issue(acq + 1u < a.fpc ? acq + 1u : acq); // lands while this acquisition packs (the last reloads)
 			if (prim) {
 				uint32_t wprev = 0u;
 				if (PRE_P == PRE_DIFF) {
@@ -603,16 +615,32 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 				a.status[fp] = size > a.cap ? ERRV(E_DST_TOO_SMALL)
 							    : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
 			}
-			lds_barrier(); // B3: the previous image was read
-			if (wid == 0u)
-				wstamp(a, acq - 1u, 4u);
-			// clear what the previous acquisition used (words 0 .. (A+31)/32 - 1,
-			// and the one after for the flush); it packs acquisition acq + 1
-			const uint32_t nw = (A_prev + 63u) >> 5;
-			for (uint32_t i = tid; i < nw; i += NT)
-				imgp[i] = 0u;
-			// (visible to the next packing: after the next step's B1)
+			if (NIMG == 2u) {
+				lds_barrier(); // B3: the previous image was read
+				if (wid == 0u)
+					wstamp(a, acq - 1u, 4u);
+				// clear what the previous acquisition used (words 0 .. (A+31)/32 - 1,
+				// and the one after for the flush); it packs acquisition acq + 1
+				const uint32_t nw = (A_prev + 63u) >> 5;
+				for (uint32_t i = tid; i < nw; i += NT)
+					imgp[i] = 0u;
+				// (visible to the next packing: after the next step's B1)
+			} else {
+				if (wid == 0u)
+					wstamp(a, acq - 1u, 4u);
+				// acquisition acq + 1 packs into the image of acquisition acq - 2,
+				// stored in step acq - 1: every wave finished that store before
+				// this step's B1.  Clear it (visible to that packing after the
+				// next step's B1)
+				if (acq >= 2u && acq + 1u < a.fpc) {
+					uint32_t *const imgn = img_at(acq + 1u);
+					const uint32_t nw = (A_prev2 + 63u) >> 5;
+					for (uint32_t i = tid; i < nw; i += NT)
+						imgn[i] = 0u;
+				}
+			}
 		}
+		A_prev2 = A_prev;
 		A_prev = A;
 		HB_prev = HB;
 		hseq_prev = hseq;
@@ -1086,7 +1114,7 @@ bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint
 bool walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
 		 bool rice_s, hipStream_t s)
 {
-	const size_t lds = (size_t)(2u * k.img_words + 8u) * 4u; // two images (walk_kernel)
+	const size_t lds = (size_t)(AIRS_WALK_NIMG * (k.img_words + 4u) + 4u) * 4u; // walk_kernel's images
 	if (sample_bytes == 2)
 		return pre_p == PRE_DIFF ? walk_launch_p<2, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
 					 : walk_launch_p<2, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);

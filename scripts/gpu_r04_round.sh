@@ -34,4 +34,10 @@ for w in $WLS; do
   python3 scripts/traffic.py $O/pf_$w/pf_results.db $O/pw_$w/pw_results.db $w $O/traffic_$w.json --kernel $K > $O/traffic_$w.log 2>&1 || { tail -3 $O/traffic_$w.log; exit 1; }
   cut -c1-300 $O/traffic_$w.json
 done
+if [ -n "$AUTO_TRACE" ]; then
+  # CMP_GPU_AUTO_RICE on cfg2-shaped frames (4 Mi samples, above the fused limit): the sliced selection's
+  # grid (select_rice_hist_kernel: one workgroup per 32 Ki-sample slice, 2048 > 16 frames)
+  AIRS_KB_AUTO=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_auto4mi -o kt -- python3 scripts/kbench.py cfg2 > $O/kt_auto4mi.log 2>&1 || { tail $O/kt_auto4mi.log; exit 1; }
+  tail -1 $O/kt_auto4mi.log
+fi
 find $O -name "*.db" -delete

@@ -36,7 +36,7 @@ BUDGETS = {
     "_ZN4airs15walk_ctx_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi4EEEvNS_5WArgsE": (128, 34),
     # the segment walk, 16 samples per lane and 8 (cfg5s8)
     "_ZN4airs11walk_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi16EEEvNS_5WArgsE": (96, 44),
-    "_ZN4airs11walk_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi8EEEvNS_5WArgsE": (72, 39),
+    "_ZN4airs11walk_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi8EEEvNS_5WArgsE": (72, 40),
 }
 
 
