@@ -92,6 +92,18 @@ struct KArgs {
 #endif
 // histogram bins: v = m + 1 in [1, 65536], bin = 8 floor(log2 v) + next 3 bits
 #define AUTO_BINS 129u
+// min(v >> k, 16) for every v of bin `bin` (top-bit position t = bin / 8, the
+// three bits after it bin % 8): 16 when k <= t - 4, 0 when k > t, else the
+// top t - k + 1 bits
+__device__ __forceinline__ uint32_t auto_term(uint32_t bin, uint32_t k)
+{
+	const uint32_t t = bin >> 3, top4 = 8u + (bin & 7u);
+	if (k + 4u <= t)
+		return 16u;
+	if (k > t)
+		return 0u;
+	return top4 >> (k + 3u - t);
+}
 
 // ---------------------------------------------------------------------
 // Golomb coder constants (reference encoder.c:185-224, with
@@ -486,6 +498,9 @@ bool walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t
 bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p,
 		     uint32_t enc_s, bool rice_s, hipStream_t s);
 uint32_t walk_ctx_samples();
+// the frame walk with the per-frame Rice k (64 Ki-sample 16-bit frames, NONE/DIFF):
+// false when the launch does not fit it
+bool frame_auto_encode(const KArgs &k, uint32_t pre, hipStream_t s);
 // samples per segment of the segment walk (walk_kernel): 4096 with four data
 // waves, 2048 with two (batches of few contexts); k.spf = n / that
 uint32_t walk_seg_samples(bool half);

@@ -60,15 +60,6 @@ __host__ __device__ constexpr uint32_t seg_images(int W, int MODEL)
 #define AIRS_AUTO_ABLATE 0
 #endif
 #define AIRS_AUTO_ABL(b) ((AIRS_AUTO_ABLATE & (b)) != 0)
-__device__ __forceinline__ uint32_t auto_term(uint32_t bin, uint32_t k)
-{
-	const uint32_t t = bin >> 3, top4 = 8u + (bin & 7u);
-	if (k + 4u <= t)
-		return 16u;
-	if (k > t)
-		return 0u;
-	return top4 >> (k + 3u - t);
-}
 
 template <int W, int PRE, int ENC, bool RICE, int MODEL, bool FULL, bool AUTO = false, bool STREAM = false>
 __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)

@@ -1131,10 +1131,22 @@ static uint32_t ensure_granules(airs_dev_engine *e, size_t segs)
 	return 0;
 }
 
+// AIRS_FAUTO=0 (env, read at each launch: A/B and tests) keeps AUTO launches
+// of 64 Ki-sample frames on the fused encode kernel
+static bool fauto_enabled()
+{
+	const char *e = getenv("AIRS_FAUTO");
+	return e ? atoi(e) != 0 : true;
+}
+
 template <int W, int PRE, int ENC, bool RICE, int MODEL>
 static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t s)
 {
 	if constexpr (ENC == ENC_ZERO && RICE && MODEL == 0 && (PRE == PRE_NONE || PRE == PRE_DIFF)) {
+		// the frame walk (64 Ki-sample frames: one workgroup per frame, no
+		// candidate granules; AIRS_FAUTO=0 keeps the fused encode kernel)
+		if (k.ktot && W == 2 && full && fauto_enabled() && frame_auto_encode(k, PRE, s))
+			return;
 		if (k.ktot && W == 2 && full && arena_auto_enabled()) { // fused Rice selection, the arena kernel
 			KArgs ka = k;
 			ka.img_words = arena_words();

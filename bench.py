@@ -531,10 +531,11 @@ def main():
     kernels = {
         "cfg2": arena + ": one launch per step",
         "cfg2s": arena + ": one launch per step, one look-back chain of 4096 segments",
-        "cfg3": ("airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO>" if os.environ.get("AIRS_ARENA_AUTO") == "0" or
-                 os.environ.get("AIRS_ARENA", "0") in ("", "0") else "airs::arena_kernel<DIFF,frames,-,AUTO>") +
-                " (the per-frame Rice k chosen in-kernel from a histogram of the samples in registers): one launch "
-                "per step",
+        "cfg3": ("airs::frame_auto_kernel<DIFF> (enc_walk.hip: one 1024-thread workgroup per 64 Ki-sample frame, "
+                 "strided; the frame's Rice k from a histogram of the samples in registers, no granules)"
+                 if os.environ.get("AIRS_FAUTO", "1") != "0" else
+                 "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO> (the per-frame Rice k chosen in-kernel from a "
+                 "histogram of the samples in registers)") + ": one launch per step",
         "cfg4": arena + ": one launch per step",
         "cfg5": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> (enc_walk.hip): ONE launch per step, one "
                 "1024-thread workgroup per stream walks its 16 acquisitions, the model in registers",

@@ -57,7 +57,7 @@ def _frames(rng, kind, n, nf, extreme):
     return out
 
 
-def _oracle(orc, orc_ext, kind, pre, frames):
+def _oracle(orc, orc_ext, kind, pre, frames, checksum=0):
     want = []
     for x in frames:
         n = x.size
@@ -65,7 +65,7 @@ def _oracle(orc, orc_ext, kind, pre, frames):
                                       pre, None)
         ctx = api.CmpContext()
         prm = P(primary_preprocessing=pre, primary_encoder_type=api.ENCODER_GOLOMB_ZERO,
-                primary_encoder_param=1 << k)
+                primary_encoder_param=1 << k, checksum_enabled=checksum)
         assert not api.is_error(orc.initialise(ctx, prm))
         cap = orc.compress_bound(2 * n)
         cap = cap if not api.is_error(cap) else 6 * n + 64  # past the 24-bit size field's worst case
@@ -76,7 +76,7 @@ def _oracle(orc, orc_ext, kind, pre, frames):
     return want
 
 
-def _gpu(prod, eng, kind, pre, frames):
+def _gpu(prod, eng, kind, pre, frames, checksum=0):
     import torch
     n, nf = frames[0].size, len(frames)
     sb = 4 if kind == "i16_in_i32" else 2
@@ -92,7 +92,8 @@ def _gpu(prod, eng, kind, pre, frames):
     sizes = torch.zeros(nf, dtype=torch.int32, device="cuda")
     ctxs = (api.CmpContext * 1)()
     # the configured g is ignored by AUTO_RICE (any valid g)
-    prm = P(primary_preprocessing=pre, primary_encoder_type=api.ENCODER_GOLOMB_ZERO, primary_encoder_param=7)
+    prm = P(primary_preprocessing=pre, primary_encoder_type=api.ENCODER_GOLOMB_ZERO, primary_encoder_param=7,
+            checksum_enabled=checksum)
     assert not api.is_error(prod.initialise(ctxs[0], prm))
     torch.cuda.synchronize()
     r = eng.compress(ctxs, nf, kind, src.data_ptr(), stride, n * sb, dst.data_ptr(), dstride, cap,
@@ -147,6 +148,31 @@ def test_autorice_arena_vs_oracle(prod, eng, orc, orc_ext, monkeypatch, kind, pr
     experiment, off by default: AIRS_ARENA=1, read at each launch)."""
     monkeypatch.setenv("AIRS_ARENA", "1")
     test_autorice_vs_oracle(prod, eng, orc, orc_ext, kind, pre, n)
+
+
+FRAME_WALK_CASES = [("u16", 1, 300, 0), ("i16", 0, 300, 1), ("u16", 0, 40, 1), ("i16", 1, 40, 0)]
+
+
+@pytest.mark.parametrize("kind,pre,nf,checksum", FRAME_WALK_CASES)
+def test_autorice_frame_walk_vs_oracle(prod, eng, orc, orc_ext, monkeypatch, kind, pre, nf, checksum):
+    """64 Ki-sample 16-bit frames take the frame walk (frame_auto_kernel: one
+    workgroup per frame, strided; 300 frames: workgroups code several frames,
+    the next frame's samples loaded while one packs): frames of every scale
+    (k = 0 .. 15), the extreme value 65535, checksums; bit-exact against the
+    oracle's rule and encoder, and equal to the fused encode kernel's frames
+    (AIRS_FAUTO=0)."""
+    rng = np.random.default_rng(zlib.crc32(f"fw/{kind}/{pre}/{nf}".encode()))
+    frames = _frames(rng, kind, 4 * SEG16, nf, extreme=True)
+    want = _oracle(orc, orc_ext, kind, pre, frames, checksum)
+    got = _gpu(prod, eng, kind, pre, frames, checksum)
+    bad = [f for f in range(nf) if _mask(got[f]) != _mask(want[f])]
+    assert not bad, (f"frames {bad[:8]} differ; g gpu/oracle "
+                     f"{[(api.parse_header(got[f])['encoder_param'], api.parse_header(want[f])['encoder_param']) for f in bad[:4]]}")
+    ks = {api.parse_header(g)["encoder_param"].bit_length() - 1 for g in got}
+    assert nf < 100 or len(ks) >= 12, sorted(ks)
+    monkeypatch.setenv("AIRS_FAUTO", "0")
+    fused = _gpu(prod, eng, kind, pre, frames, checksum)
+    assert [_mask(g) for g in fused] == [_mask(g) for g in got]
 
 
 def test_autorice_k_range(prod, eng, orc, orc_ext):

@@ -28,8 +28,11 @@ BUDGETS = {
     "_ZN4airs12arena_kernelILi1ELb0ELb0ELb1EEEvNS_5KArgsE": (96, 0),
     # cfg2 / cfg4: encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb0EEEvNS_5KArgsE": (128, 13),
-    # cfg3: encode_kernel's fused per-frame Rice selection
+    # encode_kernel's fused per-frame Rice selection (frames other than 64 Ki samples, AIRS_FAUTO=0)
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb1ELb0EEEvNS_5KArgsE": (128, 0),
+    # cfg3: the frame walk with the per-frame Rice k (1024-thread workgroups: <= 128 VGPRs)
+    "_ZN4airs17frame_auto_kernelILi1EEEvNS_5KArgsE": (128, 18),
+    "_ZN4airs17frame_auto_kernelILi0EEEvNS_5KArgsE": (128, 11),
     # cfg2s: payload-only stream
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb1EEEvNS_5KArgsE": (128, 0),
     # cfg5 / cfg5fb: the context walk (1024-thread workgroups: <= 128 VGPRs)
@@ -61,5 +64,6 @@ def test_hot_kernel_register_budget(meta, sym):
 def test_every_kernel_is_gfx950_and_listed(meta):
     names = set(meta)
     for stem in ("arena_kernel", "encode_kernel", "walk_ctx_kernel", "walk_kernel", "ck_chain_kernel",
-                 "select_rice_hist_kernel", "select_rice_pick_kernel", "fb_step_kernel", "dec_parse_kernel"):
+                 "select_rice_hist_kernel", "select_rice_pick_kernel", "fb_step_kernel", "dec_parse_kernel",
+                 "frame_auto_kernel"):
         assert any(stem in n for n in names), stem
