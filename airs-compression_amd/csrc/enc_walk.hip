@@ -279,11 +279,20 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 	// logical block index from a ticket taken at start: every
 	// workgroup with a smaller index has started (is resident or done), so a
 	// look-back only ever waits on a workgroup that is running, whatever order
-	// the XCDs dispatch in
-	if (tid == 0u)
-		s_ctl[3] = atomicAdd(a.ticket + AIRS_WALK_TICKET, 1u) - a.ticket_base;
-	__syncthreads();
-	const uint32_t lb = __builtin_amdgcn_readfirstlane(s_ctl[3]);
+	// the XCDs dispatch in.  A grid that the CUs hold at once (a.direct,
+	// host-checked occupancy) takes the block index instead: every workgroup
+	// is running, and 1024 tickets on one counter spread the workgroups'
+	// start over ~13 us (cfg5s8 with 2048-sample segments)
+	uint32_t lb = blockIdx.x;
+	if (a.direct) {
+		if (tid == 0u) // the counter still counts the launch's workgroups (no return: nothing waits)
+			__hip_atomic_fetch_add(a.ticket + AIRS_WALK_TICKET, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	} else {
+		if (tid == 0u)
+			s_ctl[3] = atomicAdd(a.ticket + AIRS_WALK_TICKET, 1u) - a.ticket_base;
+		__syncthreads();
+		lb = __builtin_amdgcn_readfirstlane(s_ctl[3]);
+	}
 	const uint32_t c = lb / a.spf, j = lb - c * a.spf;
 	const bool is_first = j == 0u, is_last = j + 1u == a.spf;
 	const uint32_t n = a.n;
@@ -1259,21 +1268,43 @@ bool frame_auto_encode(const KArgs &k, uint32_t pre, hipStream_t s)
 // ---------------------------------------------------------------------
 // launch (airs_dev_walk, airs_dev.h)
 // ---------------------------------------------------------------------
+// the segment walk's launch: the block index is the logical index when the
+// whole grid is resident at once (occupancy of this kernel x CUs), else a ticket
+template <typename K>
+static void walk_go(K kern, const WArgs &k, size_t lds, hipStream_t s)
+{
+	const uint32_t grid = k.num_ctx * k.spf;
+	static int cus = 0;
+	if (!cus) {
+		int dev = 0;
+		if (hipGetDevice(&dev) != hipSuccess ||
+		    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+			cus = -1;
+	}
+	int per_cu = 0;
+	if (cus > 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 320, lds) != hipSuccess)
+		per_cu = 0;
+	WArgs kk = k;
+	kk.direct = (cus > 0 && per_cu > 0 && (uint64_t)grid <= (uint64_t)per_cu * (uint64_t)cus) ? 1u : 0u;
+	if (const char *e = getenv("AIRS_WALK_TICKET")) // tests: 1 forces the ticket
+		kk.direct = atoi(e) ? 0u : kk.direct;
+	hipLaunchKernelGGL(kern, dim3(grid), dim3(320), lds, s, kk);
+}
+
 template <int W, int PRE_P, int ENC_P, bool RICE_P>
 static bool walk_launch_s(const WArgs &k, uint32_t enc_s, bool rice_s, size_t lds, hipStream_t s)
 {
-	const dim3 grid(k.num_ctx * k.spf);
 	const bool half = k.spf * walk_seg_samples(true) == k.n && k.spf * walk_seg_samples(false) != k.n;
 	if (enc_s == ENC_ZERO && rice_s) {
 		if (half)
-			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 8>), grid, dim3(320), lds, s, k);
+			walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 8>, k, lds, s);
 		else
-			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 16>), grid, dim3(320), lds, s, k);
+			walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 16>, k, lds, s);
 	} else if (enc_s == ENC_MULTI && rice_s) {
 		if (half)
-			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 8>), grid, dim3(320), lds, s, k);
+			walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 8>, k, lds, s);
 		else
-			hipLaunchKernelGGL((walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 16>), grid, dim3(320), lds, s, k);
+			walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 16>, k, lds, s);
 	} else {
 		return false;
 	}

@@ -1131,12 +1131,14 @@ static uint32_t ensure_granules(airs_dev_engine *e, size_t segs)
 	return 0;
 }
 
-// AIRS_FAUTO=0 (env, read at each launch: A/B and tests) keeps AUTO launches
-// of 64 Ki-sample frames on the fused encode kernel
+// AIRS_FAUTO=1 (env, read at each launch: A/B and tests) sends AUTO launches
+// of 64 Ki-sample frames to the frame walk (frame_auto_kernel); measured
+// slower than the fused encode kernel on cfg3 (78.7 against 75.0 us,
+// DESIGN.md 3.1.1), so off by default
 static bool fauto_enabled()
 {
 	const char *e = getenv("AIRS_FAUTO");
-	return e ? atoi(e) != 0 : true;
+	return e ? atoi(e) != 0 : false;
 }
 
 template <int W, int PRE, int ENC, bool RICE, int MODEL>
@@ -1144,7 +1146,7 @@ static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t 
 {
 	if constexpr (ENC == ENC_ZERO && RICE && MODEL == 0 && (PRE == PRE_NONE || PRE == PRE_DIFF)) {
 		// the frame walk (64 Ki-sample frames: one workgroup per frame, no
-		// candidate granules; AIRS_FAUTO=0 keeps the fused encode kernel)
+		// candidate granules; opt-in, AIRS_FAUTO=1)
 		if (k.ktot && W == 2 && full && fauto_enabled() && frame_auto_encode(k, PRE, s))
 			return;
 		if (k.ktot && W == 2 && full && arena_auto_enabled()) { // fused Rice selection, the arena kernel
@@ -1468,9 +1470,10 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 
 // segment-walk workgroups (of 4096 samples) below which the walk takes
 // 2048-sample segments, 8 samples per lane: twice the workgroups and waves
-// (cfg5s8: 512 -> 1024 workgroups, 2 -> 4 data waves per SIMD)
+// (cfg5s8: 512 -> 1024 workgroups, 2 -> 4 data waves per SIMD).  0 = never:
+// measured slower on cfg5s8, 83.5 against 78.7 us
 #ifndef AIRS_WALK_HALF_BELOW
-#define AIRS_WALK_HALF_BELOW 1024u
+#define AIRS_WALK_HALF_BELOW 0u
 #endif
 // contexts from which a batch of walk_ctx_samples()-sample frames takes the
 // context walk (one workgroup per context) instead of the segment walk

@@ -533,15 +533,16 @@ def main():
         "cfg2s": arena + ": one launch per step, one look-back chain of 4096 segments",
         "cfg3": ("airs::frame_auto_kernel<DIFF> (enc_walk.hip: one 1024-thread workgroup per 64 Ki-sample frame, "
                  "strided; the frame's Rice k from a histogram of the samples in registers, no granules)"
-                 if os.environ.get("AIRS_FAUTO", "1") != "0" else
+                 if os.environ.get("AIRS_FAUTO", "0") not in ("", "0") else
                  "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO> (the per-frame Rice k chosen in-kernel from a "
                  "histogram of the samples in registers)") + ": one launch per step",
         "cfg4": arena + ": one launch per step",
         "cfg5": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> (enc_walk.hip): ONE launch per step, one "
                 "1024-thread workgroup per stream walks its 16 acquisitions, the model in registers",
-        "cfg5s8": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,8> (enc_walk.hip, the segment walk): ONE launch "
-                  "per step, a 320-thread workgroup per (stream, 2048-sample segment, 8 samples per lane) walks the "
-                  "16 acquisitions, each acquisition's look-back resolved one step later",
+        "cfg5s8": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,%d> (enc_walk.hip, the segment walk): ONE launch "
+                  "per step, a 320-thread workgroup per (stream, %d-sample segment) walks the 16 acquisitions, each "
+                  "acquisition's look-back resolved one step later" %
+                  ((8, 2048) if os.environ.get("AIRS_WALK_SEG") == "2048" else (16, 4096)),
         "cfg5fb": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> with the uncompressed fallback resolved on "
                   "the chip: ONE launch per step, then one read-back of the draw counts and the identifier patch "
                   "(patch_ids_kernel)",

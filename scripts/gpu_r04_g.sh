@@ -1,0 +1,18 @@
+# Round 4: segment walk with the block index as logical index when the grid
+# is resident (no ticket): tests, timelines, A/B benches (seg x ticket).
+TAG=${1:-r04g}
+O=gpurun_out/$TAG
+cd "$GRAFT_REPO_ROOT" && mkdir -p $O && export TMPDIR=/tmp || exit 1
+timeout -k 10 700 python -u -m pytest tests/test_gpu_walk.py tests/test_gpu_batch.py tests/test_gpu_autorice.py -q \
+  --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+rc=$?; tail -3 $O/pytest.log; grep -E "^FAILED|^ERROR" $O/pytest.log | head -20
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+for seg in 4096 2048; do
+  AIRS_WALK_SEG=$seg AIRS_TS_SEG=$seg AIRS_LIB=exp/abl/libairscmp.so AIRS_WL=cfg5s8 timeout -k 10 200 python scripts/walk_ts.py $O/ts_cfg5s8_seg$seg.json > $O/ts.log 2>&1 || { tail -5 $O/ts.log; exit 1; }
+  cat $O/ts_cfg5s8_seg$seg.json | tr -d ' \n' | cut -c1-600; echo
+done
+for rep in 1 2; do for v in AIRS_WALK_SEG=4096 AIRS_WALK_SEG=2048 AIRS_WALK_SEG=4096,AIRS_WALK_TICKET=1 AIRS_WALK_SEG=2048,AIRS_WALK_TICKET=1; do
+  e=$(echo $v | tr ',' ' ')
+  env $e timeout -k 10 300 python bench.py --workload cfg5s8 --no-cpu-baseline --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; print('cfg5s8 $v', d['ms_per_step'], d['bitexact_vs_reference'], r['avg_launch_ms_hip_events'], r['frac'])"
+done; done

@@ -16,8 +16,7 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 kern() {
   case $1 in
-    cfg2|cfg2s|cfg4) echo encode_kernel ;;
-    cfg3) echo frame_auto_kernel ;;
+    cfg2|cfg2s|cfg3|cfg4) echo encode_kernel ;;
     cfg5|cfg5fb) echo walk_ctx_kernel ;;
     cfg5s8) echo walk_kernel ;;
   esac

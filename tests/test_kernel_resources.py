@@ -28,16 +28,16 @@ BUDGETS = {
     "_ZN4airs12arena_kernelILi1ELb0ELb0ELb1EEEvNS_5KArgsE": (96, 0),
     # cfg2 / cfg4: encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb0EEEvNS_5KArgsE": (128, 13),
-    # encode_kernel's fused per-frame Rice selection (frames other than 64 Ki samples, AIRS_FAUTO=0)
+    # cfg3: encode_kernel's fused per-frame Rice selection
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb1ELb0EEEvNS_5KArgsE": (128, 0),
-    # cfg3: the frame walk with the per-frame Rice k (1024-thread workgroups: <= 128 VGPRs)
+    # the frame walk with the per-frame Rice k (opt-in AIRS_FAUTO; 1024-thread workgroups: <= 128 VGPRs)
     "_ZN4airs17frame_auto_kernelILi1EEEvNS_5KArgsE": (128, 18),
     "_ZN4airs17frame_auto_kernelILi0EEEvNS_5KArgsE": (128, 11),
     # cfg2s: payload-only stream
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb1EEEvNS_5KArgsE": (128, 0),
     # cfg5 / cfg5fb: the context walk (1024-thread workgroups: <= 128 VGPRs)
     "_ZN4airs15walk_ctx_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi4EEEvNS_5WArgsE": (128, 34),
-    # the segment walk, 16 samples per lane and 8 (cfg5s8)
+    # the segment walk, 16 samples per lane (cfg5s8) and 8 (AIRS_WALK_SEG=2048)
     "_ZN4airs11walk_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi16EEEvNS_5WArgsE": (96, 44),
     "_ZN4airs11walk_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi8EEEvNS_5WArgsE": (72, 40),
 }
