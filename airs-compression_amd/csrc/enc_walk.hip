@@ -222,17 +222,30 @@ __device__ __forceinline__ void walk_pack(uint32_t *img, uint32_t excl, const ui
 			}
 		}
 	} else if (ENC == ENC_MULTI && RICE) {
+		// batches of 8 lookups issued before their puts: one at a time, each
+		// lookup waited for the LDS (and the puts before it) on its own,
+		// 16 serial LDS round trips per lane
 #pragma unroll
-		for (uint32_t j = 0; j < 2u * NP; j++) {
-			const uint32_t m = half16(mp[j >> 1], j & 1u);
-			const uint32_t off = half16(oq[j >> 1], j & 1u);
-			const uint2 e = *reinterpret_cast<const uint2 *>(tab + off);
-			if (e.y <= 32u) {
-				pk1.put(m + e.x, e.y);
-			} else { // escape longer than 32 bits: golomb(outlier + lvl), then d in 2 (lvl + 1) bits
-				const uint32_t len2 = 2u * (((31u - ((off >> 3) - 16u)) >> 1) + 1u);
-				pk1.put(e.x, e.y - len2);
-				pk1.put(m - cd.outlier, len2);
+		for (uint32_t hb = 0; hb < NP / 4u; hb++) {
+			uint2 te[8];
+#pragma unroll
+			for (uint32_t i = 0; i < 8u; i++) {
+				const uint32_t j = hb * 8u + i;
+				te[i] = *reinterpret_cast<const uint2 *>(tab + half16(oq[j >> 1], j & 1u));
+			}
+#pragma unroll
+			for (uint32_t i = 0; i < 8u; i++) {
+				const uint32_t j = hb * 8u + i;
+				const uint32_t m = half16(mp[j >> 1], j & 1u);
+				const uint2 e = te[i];
+				if (e.y <= 32u) {
+					pk1.put(m + e.x, e.y);
+				} else { // escape longer than 32 bits: golomb(outlier + lvl), then d in 2 (lvl + 1) bits
+					const uint32_t off = half16(oq[j >> 1], j & 1u);
+					const uint32_t len2 = 2u * (((31u - ((off >> 3) - 16u)) >> 1) + 1u);
+					pk1.put(e.x, e.y - len2);
+					pk1.put(m - cd.outlier, len2);
+				}
 			}
 		}
 	} else {

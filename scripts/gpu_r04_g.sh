@@ -11,8 +11,8 @@ for seg in 4096 2048; do
   AIRS_WALK_SEG=$seg AIRS_TS_SEG=$seg AIRS_LIB=exp/abl/libairscmp.so AIRS_WL=cfg5s8 timeout -k 10 200 python scripts/walk_ts.py $O/ts_cfg5s8_seg$seg.json > $O/ts.log 2>&1 || { tail -5 $O/ts.log; exit 1; }
   cat $O/ts_cfg5s8_seg$seg.json | tr -d ' \n' | cut -c1-600; echo
 done
-for rep in 1 2; do for v in AIRS_WALK_SEG=4096 AIRS_WALK_SEG=2048 AIRS_WALK_SEG=4096,AIRS_WALK_TICKET=1 AIRS_WALK_SEG=2048,AIRS_WALK_TICKET=1; do
-  e=$(echo $v | tr ',' ' ')
-  env $e timeout -k 10 300 python bench.py --workload cfg5s8 --no-cpu-baseline --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; print('cfg5s8 $v', d['ms_per_step'], d['bitexact_vs_reference'], r['avg_launch_ms_hip_events'], r['frac'])"
+for rep in 1 2; do for v in cfg5s8:AIRS_WALK_SEG=4096 cfg5s8:AIRS_WALK_SEG=2048 cfg5s8:AIRS_WALK_SEG=4096,AIRS_WALK_TICKET=1 cfg5s8:AIRS_WALK_SEG=2048,AIRS_WALK_TICKET=1 cfg5:X=1 cfg5fb:X=1; do
+  w=${v%%:*}; e=$(echo ${v#*:} | tr ',' ' ')
+  env $e timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; print('$w $e', d['ms_per_step'], d['bitexact_vs_reference'], r['avg_launch_ms_hip_events'], r['frac'], r.get('frac_samples_only'))"
 done; done
