@@ -21,12 +21,12 @@ kern() {
     cfg5s8) echo walk_kernel ;;
   esac
 }
-for w in $WLS; do
+[ -n "$SKIP_BENCH" ] || for w in $WLS; do
   cpu=--no-cpu-baseline; [ "$w" = cfg2 ] && cpu=
   timeout -k 10 400 python bench.py --workload $w $cpu > $O/bench_$w.json 2> $O/bench_$w.err || { tail $O/bench_$w.err; exit 1; }
   python3 -c "import json; d=json.load(open('$O/bench_$w.json')); r=d['roofline']; print('$w', d['ms_per_step'], d['value'], d['bitexact_vs_reference'], r['avg_launch_ms_hip_events'], r['frac'], r.get('frac_samples_only'))"
 done
-for w in $WLS; do
+[ -n "$SKIP_PROF" ] || for w in $WLS; do
   K=$(kern $w)
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$w -o kt -- python3 bench.py --workload $w --no-cpu-baseline --no-warm > $O/kt_$w.log 2>&1 || { tail $O/kt_$w.log; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pf_$w -o pf -- python3 bench.py --workload $w --steps 5 --warmup 1 --no-cpu-baseline --no-warm > $O/pf_$w.log 2>&1 || { tail -3 $O/pf_$w.log; exit 1; }
