@@ -207,6 +207,10 @@ uint32_t airs_dev_synth(struct airs_dev_engine *e, void *dst, uint32_t sample_by
 #define AIRS_NSLOT 15 /* scratch slots per engine; the last five are the device layer's (checksum
 		       * placement, checksum products, decoder parse arrays, decoder frame info, IWT heads) */
 void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes);
+/* engine-owned page-locked host scratch, grown on demand: asynchronous
+ * read-backs and uploads; the host may rewrite it once the stream has passed
+ * the copies that use it */
+void *airs_dev_host_scratch(struct airs_dev_engine *e, size_t bytes);
 
 /* rewrite header bytes 8..13 (identifier) of launch frames whose status is
  * not an error: frame j = frame_add + j*frame_mul, identifier ids[j] (device) */

@@ -1488,7 +1488,8 @@ static uint32_t batch_walk_fb(struct cmp_gpu_engine *eng, struct cmp_context *ct
 	struct airs_walk w;
 	uint32_t c, a, e = 0, seq_same = 1, m_strided = 1;
 	uint64_t mbase, mstep;
-	uint8_t *h_draws = NULL, *h_seq = NULL, *scr;
+	uint8_t *h_draws = NULL, *h_seq = NULL, *scr, *h_seq0 = NULL;
+	uint64_t *h_ids = NULL;
 
 	if (!model_needed(P) || !P->uncompressed_fallback_enabled || b->dst_capacity < raw || raw > 0xFFFFFFu ||
 	    (P->primary_preprocessing != CMP_PREPROCESS_NONE && P->primary_preprocessing != CMP_PREPROCESS_DIFF))
@@ -1554,11 +1555,18 @@ static uint32_t batch_walk_fb(struct cmp_gpu_engine *eng, struct cmp_context *ct
 		if (!airs_dev_walk_supported(&chk))
 			return WALK_NO;
 	}
-	h_draws = malloc(total);
-	h_seq = malloc(num_ctx);
-	if (!h_draws || !h_seq) {
-		e = ERRV(GENERIC);
-		goto out;
+	/* page-locked host scratch: draws [tb], final sequence numbers [num_ctx]
+	 * (one read-back of the device scratch's first tb + num_ctx bytes), then
+	 * the identifiers [total] at the next 8-byte boundary */
+	{
+		const size_t ioff = (tb + num_ctx + 7u) & ~(size_t)7u;
+		uint8_t *hp = airs_dev_host_scratch(dev, ioff + (size_t)total * 8u);
+
+		if (!hp)
+			return ERRV(GENERIC);
+		h_draws = hp;
+		h_seq = hp + tb;
+		h_ids = (uint64_t *)(void *)(hp + ioff);
 	}
 	if (!m_strided) {
 		uint64_t *hp = malloc((size_t)num_ctx * 8u), *d_ptr = airs_dev_scratch(dev, SLOT_AUX, (size_t)num_ctx * 8u);
@@ -1577,9 +1585,14 @@ static uint32_t batch_walk_fb(struct cmp_gpu_engine *eng, struct cmp_context *ct
 	if (!seq_same && !is_err(e)) {
 		uint8_t *d_seq = scr + tb + num_ctx;
 
+		h_seq0 = malloc(num_ctx);
+		if (!h_seq0) {
+			e = ERRV(GENERIC);
+			goto out;
+		}
 		for (c = 0; c < num_ctx; c++)
-			h_seq[c] = ctx[c].sequence_number;
-		e = airs_dev_h2d(dev, d_seq, h_seq, num_ctx);
+			h_seq0[c] = ctx[c].sequence_number;
+		e = airs_dev_h2d(dev, d_seq, h_seq0, num_ctx);
 		if (!is_err(e))
 			e = airs_dev_sync(dev);
 		w.seq0s = d_seq;
@@ -1592,11 +1605,10 @@ static uint32_t batch_walk_fb(struct cmp_gpu_engine *eng, struct cmp_context *ct
 	}
 	if (!is_err(e))
 		e = airs_dev_walk(dev, &w);
-	/* the one read-back: identifier draws and the final sequence numbers */
+	/* the one read-back: identifier draws and the final sequence numbers
+	 * (adjacent in the device scratch, one copy into page-locked memory) */
 	if (!is_err(e))
-		e = airs_dev_d2h(dev, h_draws, w.draws, total);
-	if (!is_err(e))
-		e = airs_dev_d2h(dev, h_seq, w.seq_out, num_ctx);
+		e = airs_dev_d2h(dev, h_draws, w.draws, tb + num_ctx);
 	if (!is_err(e))
 		e = airs_dev_sync(dev);
 	if (is_err(e))
@@ -1618,18 +1630,19 @@ static uint32_t batch_walk_fb(struct cmp_gpu_engine *eng, struct cmp_context *ct
 		ctx[c].model_size = 2u * n; /* every context's model holds a frame of this size */
 	}
 	{
+		/* upload from page-locked memory and patch, both asynchronous
+		 * (cmp_gpu_synchronize waits; the next call rewrites the host
+		 * scratch only after its own read-back, which follows them) */
 		uint64_t *d_ids = airs_dev_scratch(dev, SLOT_IDS, (size_t)total * 8u);
 
-		if (!d_ids || is_err(airs_dev_h2d(dev, d_ids, ids, (size_t)total * 8u)))
+		memcpy(h_ids, ids, (size_t)total * 8u);
+		if (!d_ids || is_err(airs_dev_h2d(dev, d_ids, h_ids, (size_t)total * 8u)))
 			e = ERRV(GENERIC);
 		else
 			e = airs_dev_patch_ids(dev, b->dst, b->dst_stride, total, 0, 1, d_ids, b->sizes);
-		if (!is_err(e))
-			e = airs_dev_sync(dev);
 	}
 out:
-	free(h_draws);
-	free(h_seq);
+	free(h_seq0);
 	return e;
 }
 

@@ -979,6 +979,8 @@ struct airs_dev_engine {
 	size_t ktot_cap;
 	uint32_t *rhist; // sliced Rice selection: 128 bins per frame
 	size_t rhist_cap; // frames
+	void *pinned; // page-locked host scratch (read-backs, identifier uploads)
+	size_t pinned_cap;
 };
 
 extern "C" int airs_dev_available(void)
@@ -1025,7 +1027,28 @@ extern "C" void airs_dev_engine_destroy(struct airs_dev_engine *e)
 	(void)hipFree(e->rhist);
 	for (int i = 0; i < AIRS_NSLOT; i++)
 		(void)hipFree(e->scratch[i]);
+	if (e->pinned)
+		(void)hipHostFree(e->pinned);
 	free(e);
+}
+
+extern "C" void *airs_dev_host_scratch(struct airs_dev_engine *e, size_t bytes)
+{
+	if (e->pinned_cap < bytes) {
+		(void)hipStreamSynchronize(e->stream); // a copy from or to the old buffer may be in flight
+		if (e->pinned)
+			(void)hipHostFree(e->pinned);
+		e->pinned = nullptr;
+		e->pinned_cap = 0;
+		const size_t want = bytes < 65536 ? 65536 : bytes + bytes / 4;
+		const hipError_t he = hipHostMalloc(&e->pinned, want, hipHostMallocDefault);
+		if (he != hipSuccess) {
+			(void)hip_fail(he, "hipHostMalloc (engine host scratch)");
+			return nullptr;
+		}
+		e->pinned_cap = want;
+	}
+	return e->pinned;
 }
 
 extern "C" void *airs_dev_engine_stream(struct airs_dev_engine *e)

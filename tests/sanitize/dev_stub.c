@@ -21,6 +21,8 @@
 struct airs_dev_engine {
 	void *scratch[AIRS_NSLOT];
 	size_t cap[AIRS_NSLOT];
+	void *pinned;
+	size_t pinned_cap;
 	uint64_t salt;
 };
 
@@ -54,6 +56,7 @@ void airs_dev_engine_destroy(struct airs_dev_engine *e)
 		return;
 	for (int i = 0; i < AIRS_NSLOT; i++)
 		free(e->scratch[i]);
+	free(e->pinned);
 	free(e);
 }
 
@@ -73,6 +76,18 @@ void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes)
 		e->cap[slot] = e->scratch[slot] ? bytes : 0;
 	}
 	return e->scratch[slot];
+}
+
+void *airs_dev_host_scratch(struct airs_dev_engine *e, size_t bytes)
+{
+	if (!e)
+		return NULL;
+	if (bytes > e->pinned_cap) {
+		free(e->pinned);
+		e->pinned = malloc(bytes);
+		e->pinned_cap = e->pinned ? bytes : 0;
+	}
+	return e->pinned;
 }
 
 uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L)
