@@ -492,7 +492,9 @@ struct WArgs {
 	uint32_t dbg;    // ablation builds: AIRS_DBG switches (0 in production)
 	uint64_t *dbgts; // AIRS_DBG bit 65536: 8 realtime stamps per (workgroup, acquisition)
 };
-bool walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
+// the segment walk: < 0 no kernel for these passes; 0 launched with the
+// ticket (the caller advances its ticket base); 1 launched direct
+int walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
 		 bool rice_s, hipStream_t s);
 // one context per workgroup (frames of walk_ctx_samples() samples); img_words
 // = words of ONE of its two 16384-sample images

@@ -296,11 +296,11 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 	// host-checked occupancy) takes the block index instead: every workgroup
 	// is running, and 1024 tickets on one counter spread the workgroups'
 	// start over ~13 us (cfg5s8 with 2048-sample segments)
+	// (A direct launch does not touch the counter at all: even an atomic
+	// without return is older than the workgroup's first sample loads, and
+	// vmcnt completes in order, so their wait included the counter's queue.)
 	uint32_t lb = blockIdx.x;
-	if (a.direct) {
-		if (tid == 0u) // the counter still counts the launch's workgroups (no return: nothing waits)
-			__hip_atomic_fetch_add(a.ticket + AIRS_WALK_TICKET, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-	} else {
+	if (!a.direct) {
 		if (tid == 0u)
 			s_ctl[3] = atomicAdd(a.ticket + AIRS_WALK_TICKET, 1u) - a.ticket_base;
 		__syncthreads();
@@ -1284,7 +1284,7 @@ bool frame_auto_encode(const KArgs &k, uint32_t pre, hipStream_t s)
 // the segment walk's launch: the block index is the logical index when the
 // whole grid is resident at once (occupancy of this kernel x CUs), else a ticket
 template <typename K>
-static void walk_go(K kern, const WArgs &k, size_t lds, hipStream_t s)
+static int walk_go(K kern, const WArgs &k, size_t lds, hipStream_t s)
 {
 	const uint32_t grid = k.num_ctx * k.spf;
 	static int cus = 0;
@@ -1302,26 +1302,21 @@ static void walk_go(K kern, const WArgs &k, size_t lds, hipStream_t s)
 	if (const char *e = getenv("AIRS_WALK_TICKET")) // tests: 1 forces the ticket
 		kk.direct = atoi(e) ? 0u : kk.direct;
 	hipLaunchKernelGGL(kern, dim3(grid), dim3(320), lds, s, kk);
+	return kk.direct ? 1 : 0;
 }
 
+// < 0: no kernel for these passes; 0: launched with the ticket; 1: direct
 template <int W, int PRE_P, int ENC_P, bool RICE_P>
-static bool walk_launch_s(const WArgs &k, uint32_t enc_s, bool rice_s, size_t lds, hipStream_t s)
+static int walk_launch_s(const WArgs &k, uint32_t enc_s, bool rice_s, size_t lds, hipStream_t s)
 {
 	const bool half = k.spf * walk_seg_samples(true) == k.n && k.spf * walk_seg_samples(false) != k.n;
-	if (enc_s == ENC_ZERO && rice_s) {
-		if (half)
-			walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 8>, k, lds, s);
-		else
-			walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 16>, k, lds, s);
-	} else if (enc_s == ENC_MULTI && rice_s) {
-		if (half)
-			walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 8>, k, lds, s);
-		else
-			walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 16>, k, lds, s);
-	} else {
-		return false;
-	}
-	return true;
+	if (enc_s == ENC_ZERO && rice_s)
+		return half ? walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 8>, k, lds, s)
+			    : walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 16>, k, lds, s);
+	if (enc_s == ENC_MULTI && rice_s)
+		return half ? walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 8>, k, lds, s)
+			    : walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 16>, k, lds, s);
+	return -1;
 }
 
 // samples per segment of the segment walk: 256 lanes of 16 samples, or of 8
@@ -1331,14 +1326,14 @@ uint32_t walk_seg_samples(bool half)
 }
 
 template <int W, int PRE_P>
-static bool walk_launch_p(const WArgs &k, uint32_t enc_p, bool rice_p, uint32_t enc_s, bool rice_s, size_t lds,
-			  hipStream_t s)
+static int walk_launch_p(const WArgs &k, uint32_t enc_p, bool rice_p, uint32_t enc_s, bool rice_s, size_t lds,
+			 hipStream_t s)
 {
 	if (enc_p == ENC_ZERO && rice_p)
 		return walk_launch_s<W, PRE_P, ENC_ZERO, true>(k, enc_s, rice_s, lds, s);
 	if (enc_p == ENC_MULTI && rice_p)
 		return walk_launch_s<W, PRE_P, ENC_MULTI, true>(k, enc_s, rice_s, lds, s);
-	return false;
+	return -1;
 }
 
 template <int W, int PRE_P, int ENC_P, bool RICE_P>
@@ -1383,8 +1378,8 @@ bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint
 				 : walk_ctx_launch_p<4, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);
 }
 
-bool walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
-		 bool rice_s, hipStream_t s)
+int walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
+		bool rice_s, hipStream_t s)
 {
 	const size_t lds = (size_t)(AIRS_WALK_NIMG * (k.img_words + 4u) + 4u) * 4u; // walk_kernel's images
 	if (sample_bytes == 2)

@@ -1493,10 +1493,11 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 
 // segment-walk workgroups (of 4096 samples) below which the walk takes
 // 2048-sample segments, 8 samples per lane: twice the workgroups and waves
-// (cfg5s8: 512 -> 1024 workgroups, 2 -> 4 data waves per SIMD).  0 = never:
-// measured slower on cfg5s8, 83.5 against 78.7 us
+// (cfg5s8: 512 -> 1024 workgroups, 2 -> 4 data waves per SIMD): 67.8-68.6
+// against 70.0-70.8 us once direct launches stopped touching the ticket
+// counter
 #ifndef AIRS_WALK_HALF_BELOW
-#define AIRS_WALK_HALF_BELOW 0u
+#define AIRS_WALK_HALF_BELOW 1024u
 #endif
 // contexts from which a batch of walk_ctx_samples()-sample frames takes the
 // context walk (one workgroup per context) instead of the segment walk
@@ -1628,10 +1629,12 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 	}
 #endif
 	k.ticket_base = e->walk_ticket_base;
-	if (!walk_encode(k, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream))
+	const int wr = walk_encode(k, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream);
+	if (wr < 0)
 		return ERRV(E_PARAMS_INVALID);
 	HIPCHECK(hipGetLastError());
-	e->walk_ticket_base += (uint32_t)(w->num_ctx * spf);
+	if (wr == 0) // the launch took tickets
+		e->walk_ticket_base += (uint32_t)(w->num_ctx * spf);
 	return 0;
 }
 

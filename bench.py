@@ -542,7 +542,7 @@ def main():
         "cfg5s8": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,%d> (enc_walk.hip, the segment walk): ONE launch "
                   "per step, a 320-thread workgroup per (stream, %d-sample segment) walks the 16 acquisitions, each "
                   "acquisition's look-back resolved one step later" %
-                  ((8, 2048) if os.environ.get("AIRS_WALK_SEG") == "2048" else (16, 4096)),
+                  ((16, 4096) if os.environ.get("AIRS_WALK_SEG") == "4096" else (8, 2048)),
         "cfg5fb": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> with the uncompressed fallback resolved on "
                   "the chip: ONE launch per step, then one read-back of the draw counts and the identifier patch "
                   "(patch_ids_kernel)",
