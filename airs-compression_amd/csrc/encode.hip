@@ -1514,6 +1514,9 @@ static uint32_t ctx_walk_words(const struct airs_walk *w)
 	const uint32_t mbs = code_max_bits(w->enc_s, w->g_s, w->outl_s);
 	const uint32_t mb = mbp > mbs ? mbp : mbs;
 	const uint32_t cw = ((walk_ctx_samples() / 4u * mb / 32u + 8u) + 3u) & ~3u;
+	if (const char *e = getenv("AIRS_WALK_CTX")) // A/B: 0 sends these batches to the segment walk
+		if (!atoi(e) && !w->fb)
+			return 0u;
 	if (w->n == walk_ctx_samples() && w->num_ctx >= AIRS_WALK_CTX_MIN && (2u * cw + 4u) * 4u <= 150u * 1024u)
 		return cw;
 	return 0u;
