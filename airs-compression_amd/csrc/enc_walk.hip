@@ -46,11 +46,13 @@ namespace airs {
 
 // rows of the code tables in LDS (one table per pass)
 #define WTAB 48u
-// LDS images of the segment walk (2: a third barrier per step clears the
-// image of the acquisition just stored; 3: no third barrier)
-#ifndef AIRS_WALK_NIMG
-#define AIRS_WALK_NIMG 3u
+// The segment walk stores acquisition a in step a + LAG, and keeps LAG + 2
+// LDS images: acquisition a + 1 packs into the image stored two steps
+// earlier, so no barrier clears the one just stored
+#ifndef AIRS_WALK_LAG
+#define AIRS_WALK_LAG 1u
 #endif
+#define AIRS_WALK_NIMG (AIRS_WALK_LAG + 2u)
 
 // table entry idx of a pass: {T, len}; see the header comment
 template <int ENC>
@@ -316,7 +318,9 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 	// into image a % NIMG and is stored in the next step, once its frame
 	// offset is known.  With three, the image acquisition a + 1 packs into was
 	// stored two steps earlier, so it is cleared without a third barrier
+	constexpr uint32_t LAG = AIRS_WALK_LAG;
 	constexpr uint32_t NIMG = AIRS_WALK_NIMG;
+	static_assert((LAG == 1u || LAG == 2u) && NIMG == LAG + 2u, "images: the lag plus two");
 	auto img_at = [&](uint32_t q) { return L_img + 4u + (q % NIMG) * (a.img_words + 4u); };
 
 	const Coder cp = make_coder<ENC_P>(ENC_P == ENC_RAW ? 1u : a.g_p, a.outl_p);
@@ -379,111 +383,112 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 
 	const char *tab_p = reinterpret_cast<const char *>(s_tab[0]);
 	const char *tab_s = reinterpret_cast<const char *>(s_tab[1]);
-	uint32_t sq = seq0;
-	// the previous acquisition (packed, waiting for its frame offset)
-	uint32_t A_prev = 0u, A_prev2 = 0u, HB_prev = 0u, hseq_prev = 0u;
-	bool prim_prev = false;
 	// Step `acq` codes acquisition acq (acq < fpc) and stores acquisition
-	// acq - 1 (acq > 0).  The look-back of acquisition acq - 1 runs in step acq:
-	// every segment published its aggregate and tail for it one step earlier,
-	// so it is one granule round trip (look-back window and tail together),
-	// issued before B1 and overlapped with phase 1 and the packing, and never
-	// waits on a chain of predecessors.
-	for (uint32_t acq = 0; acq <= a.fpc; acq++) {
-		const bool have = acq < a.fpc, prev = acq > 0u;
-		const uint32_t f = c * a.fpc + acq;
-		const bool prim = sq == 0u || sq > a.iters; // cmp.c:228-248
-		const uint32_t hseq = prim ? 0u : sq;
-		if (have)
-			sq = prim ? 1u : sq + 1u;
-		const uint32_t HB = prim ? hdr_bits(PRE_P, ENC_P) : hdr_bits(PRE_MODEL, ENC_S);
-		uint32_t *const img = img_at(acq);
-		uint32_t *const imgp = img_at(acq + NIMG - 1u);
-		uint32_t mp[E / 2], oq[E / 2];
-		uint32_t T = 0u, excl = 0u;
-		if (have && data) {
-			// ---- phase 1: samples, residuals, model update, lengths ----------
-			uint32_t w[E / 2];
-			if (W == 2) {
+	// acq - LAG (acq >= LAG).  The look-back of acquisition acq - LAG runs in
+	// step acq: every segment published its aggregate and tail for it LAG
+	// steps earlier, so it is one granule round trip (look-back window and
+	// tail together, issued at the end of the step before), and it never
+	// waits on a chain of predecessors; with LAG = 2 it has a whole step to
+	// return, so the control wave is not what the step's B2 waits for.
+	//
+	// The data waves and the control wave run separate copies of the step loop
+	// (same barriers, B1 and B2 per step).  In one shared loop the compiler's
+	// wait analysis merged the control wave's granule loads into the data
+	// waves' paths and made the data waves wait for everything outstanding
+	// (their own sample prefetch included) before the store.  The data waves'
+	// output stores are a fixed number per step (past the capacity when there
+	// is nothing to store: dropped by the buffer range check), so the wait for
+	// the next step's samples counts exactly the stores issued after them.
+	uint32_t sq = seq0;
+	if (data) {
+		// the first samples and the model in registers before the loop: the
+		// loop head then has the same outstanding operations on entry as from
+		// its back edge (the step's stores), and the compiler's wait there
+		// need not cover them (vmcnt(0), expcnt and lgkmcnt left alone)
+		__builtin_amdgcn_s_waitcnt(0x0F70);
+		uint32_t A1 = 0u, A2 = 0u, A3 = 0u; // the bit totals of acquisitions acq - 1, acq - 2, acq - 3
+		// quads of one image per data thread, at most (48-bit codewords)
+		constexpr uint32_t NQ = (SEGW * 48u / 32u / 4u + 2u + ND - 1u) / ND;
+		for (uint32_t acq = 0; acq < a.fpc + LAG; acq++) {
+			const bool have = acq < a.fpc, prev = acq >= LAG;
+			const uint32_t f = c * a.fpc + acq;
+			const bool prim = sq == 0u || sq > a.iters; // cmp.c:228-248
+			if (have)
+				sq = prim ? 1u : sq + 1u;
+			uint32_t *const img = img_at(acq);
+			uint32_t *const imgp = img_at(acq + NIMG - LAG); // acquisition acq - LAG
+			uint32_t mp[E / 2], oq[E / 2];
+			uint32_t T = 0u, excl = 0u;
+			if (have) {
+				// ---- phase 1: samples, residuals, model update, lengths ----------
+				uint32_t w[E / 2];
+				if (W == 2) {
 #pragma unroll
-				for (uint32_t q = 0; q < RW; q++) {
-					w[4 * q] = rn[q].x ^ flip;
-					w[4 * q + 1] = rn[q].y ^ flip;
-					w[4 * q + 2] = rn[q].z ^ flip;
-					w[4 * q + 3] = rn[q].w ^ flip;
-				}
-			} else {
+					for (uint32_t q = 0; q < RW; q++) {
+						w[4 * q] = rn[q].x ^ flip;
+						w[4 * q + 1] = rn[q].y ^ flip;
+						w[4 * q + 2] = rn[q].z ^ flip;
+						w[4 * q + 3] = rn[q].w ^ flip;
+					}
+				} else {
 #pragma unroll
-				for (uint32_t q = 0; q < RW; q++) {
-					w[2 * q] = __builtin_amdgcn_perm(rn[q].y, rn[q].x, 0x05040100u) ^ flip;
-					w[2 * q + 1] = __builtin_amdgcn_perm(rn[q].w, rn[q].z, 0x05040100u) ^ flip;
+					for (uint32_t q = 0; q < RW; q++) {
+						w[2 * q] = __builtin_amdgcn_perm(rn[q].y, rn[q].x, 0x05040100u) ^ flip;
+						w[2 * q + 1] = __builtin_amdgcn_perm(rn[q].w, rn[q].z, 0x05040100u) ^ flip;
+					}
 				}
+				if (wid == 0u)
+					wstamp(a, acq, 0u);
+				const uint32_t prevs = first ? pn & 0xFFFFu : 0u;
+				issue(acq + 1u < a.fpc ? acq + 1u : acq); // lands while this acquisition packs (the last reloads)
+				if (prim) {
+					uint32_t wprev = 0u;
+					if (PRE_P == PRE_DIFF) {
+						wprev = __shfl_up(w[E / 2 - 1], 1, 64);
+						if (lane == 0u)
+							wprev = (prevs << 16) ^ flip;
+					}
+#pragma unroll
+					for (uint32_t q = 0; q < E / 2; q++) {
+						uint32_t u = w[q] ^ flip; // NONE: the sample itself
+						if (PRE_P == PRE_DIFF)
+							u = unpk(pk(w[q]) - pk(__builtin_amdgcn_alignbit(w[q], q ? w[q - 1] : wprev, 16)));
+						mp[q] = ENC_P == ENC_RAW ? u : zigzag_pk(u);
+						mdl[q] = w[q]; // cmp.c:305-306: the model takes the samples
+					}
+					T = walk_lengths<ENC_P, RICE_P>(mp, oq, cp, fast_p, tab_p);
+				} else {
+					const int32_t r1 = 16 - (int32_t)a.model_rate;
+#pragma unroll
+					for (uint32_t q = 0; q < E / 2; q++) {
+						const uint32_t u = unpk(pk(w[q]) - pk(mdl[q])); // preprocess.c:406-411
+						mp[q] = ENC_S == ENC_RAW ? u : zigzag_pk(u);
+						mdl[q] = model_update_zx(w[q], mdl[q], r1); // cmp.c:132-142
+					}
+					T = walk_lengths<ENC_S, RICE_S>(mp, oq, cs, fast_s, tab_s);
+				}
+#pragma unroll
+				for (uint32_t q = 0; q < E / 2; q++)
+					asm volatile("" : "+v"(mp[q]), "+v"(oq[q]));
+				const uint32_t inc = wave_incl_scan(T);
+				if (lane == 63u)
+					s_wsum[wid] = inc;
+				excl = inc - T;
 			}
+			lds_barrier(); // B1: wave totals
+			uint32_t Asum = 0u, wpre = 0u;
+#pragma unroll
+			for (uint32_t w = 0; w < DW; w++) {
+				const uint32_t v = s_wsum[w];
+				wpre += w < wid ? v : 0u;
+				Asum += v;
+			}
+			const uint32_t A = have ? __builtin_amdgcn_readfirstlane(Asum) : 0u;
 			if (wid == 0u)
-				wstamp(a, acq, 0u);
-			const uint32_t prevs = first ? pn & 0xFFFFu : 0u;
-			issue(acq + 1u < a.fpc ? acq + 1u : acq); // lands while this acquisition packs (the last reloads)
-			if (prim) {
-				uint32_t wprev = 0u;
-				if (PRE_P == PRE_DIFF) {
-					wprev = __shfl_up(w[E / 2 - 1], 1, 64);
-					if (lane == 0u)
-						wprev = (prevs << 16) ^ flip;
-				}
-#pragma unroll
-				for (uint32_t q = 0; q < E / 2; q++) {
-					uint32_t u = w[q] ^ flip; // NONE: the sample itself
-					if (PRE_P == PRE_DIFF)
-						u = unpk(pk(w[q]) - pk(__builtin_amdgcn_alignbit(w[q], q ? w[q - 1] : wprev, 16)));
-					mp[q] = ENC_P == ENC_RAW ? u : zigzag_pk(u);
-					mdl[q] = w[q]; // cmp.c:305-306: the model takes the samples
-				}
-				T = walk_lengths<ENC_P, RICE_P>(mp, oq, cp, fast_p, tab_p);
-			} else {
-				const int32_t r1 = 16 - (int32_t)a.model_rate;
-#pragma unroll
-				for (uint32_t q = 0; q < E / 2; q++) {
-					const uint32_t u = unpk(pk(w[q]) - pk(mdl[q])); // preprocess.c:406-411
-					mp[q] = ENC_S == ENC_RAW ? u : zigzag_pk(u);
-					mdl[q] = model_update_zx(w[q], mdl[q], r1); // cmp.c:132-142
-				}
-				T = walk_lengths<ENC_S, RICE_S>(mp, oq, cs, fast_s, tab_s);
-			}
-#pragma unroll
-			for (uint32_t q = 0; q < E / 2; q++)
-				asm volatile("" : "+v"(mp[q]), "+v"(oq[q]));
-			const uint32_t inc = wave_incl_scan(T);
-			if (lane == 63u)
-				s_wsum[wid] = inc;
-			excl = inc - T;
-		}
-		// control wave: the first look-back round of acquisition acq - 1 and its
-		// predecessor tail, issued together now and evaluated after B1 (one round
-		// trip, overlapped with phase 1; the segments before it published both
-		// during the previous step)
-		uint64_t gv0 = 0ull, tv0 = 0ull;
-		if (!data && prev && !is_first) {
-			const uint64_t gseg = (uint64_t)(f - 1u) * a.spf + j;
-			const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane;
-			if (lane == 0u)
-				tv0 = gran_load(&a.tail[gseg - 1u]);
-			gv0 = idx >= (int64_t)(gseg - j) ? gran_load(&a.agg[idx]) : 0ull;
-		}
-		lds_barrier(); // B1: wave totals
-		uint32_t Asum = 0u, wpre = 0u;
-#pragma unroll
-		for (uint32_t w = 0; w < DW; w++) {
-			const uint32_t v = s_wsum[w];
-			wpre += w < wid ? v : 0u;
-			Asum += v;
-		}
-		const uint32_t A = have ? __builtin_amdgcn_readfirstlane(Asum) : 0u;
-		if (wid == 0u)
-			wstamp(a, acq < a.fpc ? acq : a.fpc - 1u, 1u);
-		if (data) {
+				wstamp(a, acq < a.fpc ? acq : a.fpc - 1u, 1u);
 			if (have) {
 				excl += wpre;
-				// ---- pack into this acquisition's image -------------------------
+				// ---- pack into this acquisition's image -----------------------------
 				if (prim)
 					walk_pack<ENC_P, RICE_P>(img, excl, mp, oq, cp, fast_p, tab_p);
 				else
@@ -497,20 +502,102 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 					if (lane == 0u)
 						gran_store(&a.tail[(uint64_t)f * a.spf + j], ((uint64_t)a.epoch << 32) | tl);
 				}
+				if (wid == 0u)
+					wstamp(a, acq, 2u);
 			}
-		} else {
-			// ---- control wave: this step's aggregate, the previous step's
-			// look-back and predecessor tail ---------------------------------
+			lds_barrier(); // B2: this step's image packed; the previous step's offset and predecessor bits
+			// ---- store acquisition acq - LAG: funnel shift to the frame bit
+			// offset, big-endian; NQ + 1 stores per thread in every step -------
+			{
+				const uint32_t A_st = LAG == 2u ? A2 : A1;
+				const uint32_t P = __builtin_amdgcn_readfirstlane(s_ctl[0]);
+				const uint32_t pred = __builtin_amdgcn_readfirstlane(s_ctl[1]);
+				const uint32_t r = P & 31u, g0 = P >> 5;
+				const uint32_t endbit = P + A_st;
+				const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
+				const uint32_t nfull = prev ? ((endbit & 31u) == 0u ? J + 1u : J) : 0u;
+				uint8_t *fdst = a.dst + (uint64_t)(prev ? f - LAG : f) * a.dst_stride;
+				const __amdgpu_buffer_rsrc_t dst_rsrc =
+					__builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(a.cap & ~3u), 0x00020000);
+				const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)imgp);
+				const uint32_t nquad = nfull >> 2;
+#pragma unroll
+				for (uint32_t i = 0; i < NQ; i++) {
+					const uint32_t p = tid + i * ND;
+					const bool in = p < nquad;
+					const uint32_t jw = in ? 4u * p : 0u;
+					const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + jw);
+					const uint32_t hi = jw ? Ll[jw - 1u] : pred;
+					u32x4 o;
+					o.x = bswap32(__builtin_amdgcn_alignbit(hi, wv.x, r));
+					o.y = bswap32(__builtin_amdgcn_alignbit(wv.x, wv.y, r));
+					o.z = bswap32(__builtin_amdgcn_alignbit(wv.y, wv.z, r));
+					o.w = bswap32(__builtin_amdgcn_alignbit(wv.z, wv.w, r));
+					// past the buffer range when there is nothing to store: dropped
+					__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, in ? (int)(4u * (g0 + jw)) : INT32_MIN, 0, 0);
+				}
+				const uint32_t rr = (tid - nquad) & (ND - 1u);
+				const bool part = rr < (nfull & 3u);
+				const uint32_t jw = part ? 4u * nquad + rr : 0u;
+				const uint32_t hi = jw ? Ll[jw - 1u] : pred;
+				const uint32_t v = __builtin_amdgcn_alignbit(hi, Ll[jw], r);
+				__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, part ? (int)(4u * (g0 + jw)) : INT32_MIN, 0,
+								      0);
+				if (prev && wid == 0u)
+					wstamp(a, acq - LAG, 4u);
+			}
+			// acquisition acq + 1 packs into the image of acquisition
+			// acq + 1 - NIMG = acq - LAG - 1, stored in step acq - 1: every wave
+			// finished that store before this step's B1.  Clear it (visible to
+			// that packing after the next B1)
+			if (acq >= LAG + 1u && acq + 1u < a.fpc) {
+				uint32_t *const imgn = img_at(acq + 1u);
+				const uint32_t nw = ((LAG == 2u ? A3 : A2) + 63u) >> 5;
+				for (uint32_t i = tid; i < nw; i += ND)
+					imgn[i] = 0u;
+			}
+			A3 = A2;
+			A2 = A1;
+			A1 = A;
+		}
+	} else {
+		// ---- the control wave: aggregates, look-backs, predecessor tails,
+		// frame epilogues ----------------------------------------------------
+		// acquisitions acq - 1 and acq - 2: bit total, header bits, header
+		// sequence number, primary pass
+		uint32_t A1 = 0u, HB1 = 0u, hseq1 = 0u, A2 = 0u, HB2 = 0u, hseq2 = 0u;
+		bool prim1 = false, prim2 = false;
+		// the first look-back round of the acquisition to store next step and
+		// its predecessor tail, issued at the end of the step before, evaluated
+		// after B1
+		uint64_t gv0 = 0ull, tv0 = 0ull;
+		for (uint32_t acq = 0; acq < a.fpc + LAG; acq++) {
+			const bool have = acq < a.fpc, prev = acq >= LAG;
+			const uint32_t f = c * a.fpc + acq;
+			const bool prim = sq == 0u || sq > a.iters; // cmp.c:228-248
+			const uint32_t hseq = prim ? 0u : sq;
+			if (have)
+				sq = prim ? 1u : sq + 1u;
+			const uint32_t HB = prim ? hdr_bits(PRE_P, ENC_P) : hdr_bits(PRE_MODEL, ENC_S);
+			lds_barrier(); // B1: wave totals
+			uint32_t Asum = 0u;
+#pragma unroll
+			for (uint32_t w = 0; w < DW; w++)
+				Asum += s_wsum[w];
+			const uint32_t A = have ? __builtin_amdgcn_readfirstlane(Asum) : 0u;
 			if (have && lane == 0u) {
 				const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
 				gran_store(&a.agg[(uint64_t)f * a.spf + j], (tag << 32) | (is_first ? HB + A : A));
 			}
+			const uint32_t A_st = LAG == 2u ? A2 : A1, HB_st = LAG == 2u ? HB2 : HB1;
+			const uint32_t hseq_st = LAG == 2u ? hseq2 : hseq1;
+			const bool prim_st = LAG == 2u ? prim2 : prim1;
+			uint32_t P = HB_st, pred = 0u;
 			if (prev) {
-				const uint64_t gseg = (uint64_t)(f - 1u) * a.spf + j;
-				uint32_t P = HB_prev, pred = 0u;
+				const uint64_t gseg = (uint64_t)(f - LAG) * a.spf + j;
 				if (is_first) {
-					const uint32_t enc = prim_prev ? ENC_P : ENC_S;
-					pred = (enc != ENC_RAW) ? ((prim_prev ? cp.outlier : cs.outlier) & 0xFFFFu) : 0u;
+					const uint32_t enc = prim_st ? ENC_P : ENC_S;
+					pred = (enc != ENC_RAW) ? ((prim_st ? cp.outlier : cs.outlier) & 0xFFFFu) : 0u;
 				} else {
 					const uint64_t first_seg = gseg - j;
 					uint32_t sum = 0u, spins = 0u;
@@ -544,8 +631,8 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 					}
 					P = sum;
 					if (lane == 0u)
-						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (P + A_prev));
-					wstamp(a, acq - 1u, 5u);
+						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (P + A_st));
+					wstamp(a, acq - LAG, 5u);
 					// the predecessor's last 32 bits (published after its packing)
 					uint64_t tv = tv0;
 					if (lane == 0u) {
@@ -559,52 +646,23 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 						}
 					}
 					pred = (uint32_t)__shfl(tv, 0, 64);
-					wstamp(a, acq - 1u, 6u);
+					wstamp(a, acq - LAG, 6u);
 				}
 				if (lane == 0u) {
 					s_ctl[0] = P;
 					s_ctl[1] = pred;
 				}
 			}
-		}
-		if (wid == 0u && have)
-			wstamp(a, acq, 2u);
-		lds_barrier(); // B2: this step's image packed; the previous step's offset and predecessor bits
-		if (prev) {
-			const uint32_t fp = f - 1u;
-			const uint32_t P = __builtin_amdgcn_readfirstlane(s_ctl[0]);
-			const uint32_t pred = __builtin_amdgcn_readfirstlane(s_ctl[1]);
-			const uint32_t r = P & 31u, g0 = P >> 5;
-			const uint32_t endbit = P + A_prev;
-			const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
-			const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
-			uint8_t *fdst = a.dst + (uint64_t)fp * a.dst_stride;
-			const __amdgpu_buffer_rsrc_t dst_rsrc =
-				__builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(a.cap & ~3u), 0x00020000);
-			if (data) {
-				// ---- store: funnel shift to the frame bit offset, big-endian ------
-				const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)imgp);
-				const uint32_t nquad = nfull >> 2;
-				for (uint32_t p = tid; p < nquad; p += ND) {
-					const uint32_t jw = 4u * p;
-					const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + jw);
-					const uint32_t hi = jw ? Ll[jw - 1u] : pred;
-					u32x4 o;
-					o.x = bswap32(__builtin_amdgcn_alignbit(hi, wv.x, r));
-					o.y = bswap32(__builtin_amdgcn_alignbit(wv.x, wv.y, r));
-					o.z = bswap32(__builtin_amdgcn_alignbit(wv.y, wv.z, r));
-					o.w = bswap32(__builtin_amdgcn_alignbit(wv.z, wv.w, r));
-					__builtin_amdgcn_raw_buffer_store_b128(o, dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
-				}
-				const uint32_t rr = (tid - nquad) & (ND - 1u);
-				if (rr < (nfull & 3u)) {
-					const uint32_t jw = 4u * nquad + rr;
-					const uint32_t hi = jw ? Ll[jw - 1u] : pred;
-					const uint32_t v = __builtin_amdgcn_alignbit(hi, Ll[jw], r);
-					__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, (int)(4u * (g0 + jw)), 0, 0);
-				}
-			} else if (is_last && lane == 0u) {
+			lds_barrier(); // B2
+			if (prev && is_last && lane == 0u) {
 				// ---- frame epilogue (cmp.c:314-334) ---------------------------------
+				const uint32_t fp = f - LAG;
+				uint32_t *const imgp = img_at(acq + NIMG - LAG);
+				const uint32_t r = P & 31u, g0 = P >> 5;
+				const uint32_t endbit = P + A_st;
+				const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
+				const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
+				uint8_t *fdst = a.dst + (uint64_t)fp * a.dst_stride;
 				if (nfull == J) { // zero-padded final bytes (bitstream_flush)
 					const uint32_t hi = J ? imgp[J - 1u] : pred;
 					const uint32_t v = __builtin_amdgcn_alignbit(hi, imgp[J], r);
@@ -622,51 +680,37 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 							fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
 				}
 				const uint64_t id =
-					a.ids ? a.ids[fp] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)(acq - 1u) * a.id_astep;
+					a.ids ? a.ids[fp] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)(acq - LAG) * a.id_astep;
 				uint32_t h[5];
-				if (prim_prev)
-					header_words(h, size, 2u * n, id, hseq_prev, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
+				if (prim_st)
+					header_words(h, size, 2u * n, id, hseq_st, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
 						     ENC_P == ENC_RAW ? 0u : cp.g, ENC_P == ENC_RAW ? 0u : cp.outlier);
 				else
-					header_words(h, size, 2u * n, id, hseq_prev, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S,
+					header_words(h, size, 2u * n, id, hseq_st, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S,
 						     a.model_rate, ENC_S == ENC_RAW ? 0u : cs.g, ENC_S == ENC_RAW ? 0u : cs.outlier);
-				const uint32_t hwords = HB_prev == 176u ? 5u : 4u;
+				const uint32_t hwords = HB_st == 176u ? 5u : 4u;
 				for (uint32_t wq = 0; wq < hwords; wq++)
 					if (4u * wq + 4u <= a.cap)
 						*reinterpret_cast<uint32_t *>(fdst + 4u * wq) = bswap32(h[wq]);
 				a.status[fp] = size > a.cap ? ERRV(E_DST_TOO_SMALL)
 							    : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
 			}
-			if (NIMG == 2u) {
-				lds_barrier(); // B3: the previous image was read
-				if (wid == 0u)
-					wstamp(a, acq - 1u, 4u);
-				// clear what the previous acquisition used (words 0 .. (A+31)/32 - 1,
-				// and the one after for the flush); it packs acquisition acq + 1
-				const uint32_t nw = (A_prev + 63u) >> 5;
-				for (uint32_t i = tid; i < nw; i += NT)
-					imgp[i] = 0u;
-				// (visible to the next packing: after the next step's B1)
-			} else {
-				if (wid == 0u)
-					wstamp(a, acq - 1u, 4u);
-				// acquisition acq + 1 packs into the image of acquisition acq - 2,
-				// stored in step acq - 1: every wave finished that store before
-				// this step's B1.  Clear it (visible to that packing after the
-				// next step's B1)
-				if (acq >= 2u && acq + 1u < a.fpc) {
-					uint32_t *const imgn = img_at(acq + 1u);
-					const uint32_t nw = (A_prev2 + 63u) >> 5;
-					for (uint32_t i = tid; i < nw; i += NT)
-						imgn[i] = 0u;
-				}
+			if (acq + 1u >= LAG && acq + 1u - LAG < a.fpc && !is_first) {
+				// the look-back of acquisition acq + 1 - LAG (next step)
+				const uint64_t gseg = (uint64_t)(c * a.fpc + acq + 1u - LAG) * a.spf + j;
+				const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane;
+				tv0 = lane == 0u ? gran_load(&a.tail[gseg - 1u]) : 0ull;
+				gv0 = idx >= (int64_t)(gseg - j) ? gran_load(&a.agg[idx]) : 0ull;
 			}
+			A2 = A1;
+			HB2 = HB1;
+			hseq2 = hseq1;
+			prim2 = prim1;
+			A1 = A;
+			HB1 = HB;
+			hseq1 = hseq;
+			prim1 = prim;
 		}
-		A_prev2 = A_prev;
-		A_prev = A;
-		HB_prev = HB;
-		hseq_prev = hseq;
-		prim_prev = prim;
 	}
 	// the model after the last acquisition, to the work buffer (cmp.c:304-311)
 	if (data) {
@@ -696,6 +740,13 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 //   * two barriers per chunk: wave totals (B1), packed image (B2).
 // ---------------------------------------------------------------------
 #define CW_THREADS 1024u
+// the context walk's stores per thread and chunk (cw_chunk NQ; two images of
+// at most 150 KiB, ctx_walk_words, hold < 4.7 quads per thread, so 5 would
+// do): 0, the uncounted asm stores, because 5 counted ones took the kernel to
+// 128 VGPRs with scratch spills
+#ifndef CW_NQ
+#define CW_NQ 0u
+#endif
 #define CW_WAVES (CW_THREADS / 64u)
 #define CW_CHUNK (CW_THREADS * EPT)
 // register sets of prefetched samples (1: the next chunk is loaded while one
@@ -755,7 +806,15 @@ struct CwState {
 // offset mod 32 into img (the carry ORed into word 0), B2, store of the whole
 // words (frame word (P >> 5) + i, big-endian), carry of the partial last
 // word; the previous chunk's image imgo is cleared after B1.
-template <int ENC, bool RICE, uint32_t NT = CW_THREADS>
+//
+// NQ = 0: the stores are inline asm, uncounted by the compiler (a loop of
+// data-dependent length).  NQ > 0: exactly NQ 16-byte stores and one 4-byte
+// store per thread, those with nothing to store past the buffer range
+// (dropped), as compiler builtins: the compiler then counts them, and its
+// wait for a prefetch issued before them lets them stay in flight (with NQ =
+// 0 that wait, vmcnt(n) for the n loads it knows of, also waited for the
+// uncounted stores, which are younger).  Needs NQ * NT quads >= any chunk's.
+template <int ENC, bool RICE, uint32_t NT = CW_THREADS, uint32_t NQ = 0u>
 __device__ __forceinline__ void cw_chunk(CwState &st, uint32_t *img, uint32_t *imgo, uint32_t (*s_wsum)[NT / 64u],
 					 uint32_t par, uint32_t T, const uint32_t (&mp)[EPT / 2],
 					 const uint32_t (&oq)[EPT / 2], const Coder &cd, bool fast, const char *tab,
@@ -782,19 +841,41 @@ __device__ __forceinline__ void cw_chunk(CwState &st, uint32_t *img, uint32_t *i
 	const uint32_t end = r + A, nfull = end >> 5;
 	const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)img);
 	const uint32_t g0 = st.P >> 5;
-	for (uint32_t p = tid; p < (nfull >> 2); p += NT) {
-		const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + 4u * p);
-		u32x4 o;
-		o.x = bswap32(wv.x);
-		o.y = bswap32(wv.y);
-		o.z = bswap32(wv.z);
-		o.w = bswap32(wv.w);
-		store_b128_nc(o, 4u * (g0 + 4u * p), dst_rsrc);
-	}
-	const uint32_t rr = (tid - (nfull >> 2)) & (NT - 1u);
-	if (rr < (nfull & 3u)) {
-		const uint32_t jw = (nfull & ~3u) + rr;
-		store_b32_nc(bswap32(Ll[jw]), 4u * (g0 + jw), dst_rsrc);
+	if constexpr (NQ == 0u) {
+		for (uint32_t p = tid; p < (nfull >> 2); p += NT) {
+			const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + 4u * p);
+			u32x4 o;
+			o.x = bswap32(wv.x);
+			o.y = bswap32(wv.y);
+			o.z = bswap32(wv.z);
+			o.w = bswap32(wv.w);
+			store_b128_nc(o, 4u * (g0 + 4u * p), dst_rsrc);
+		}
+		const uint32_t rr = (tid - (nfull >> 2)) & (NT - 1u);
+		if (rr < (nfull & 3u)) {
+			const uint32_t jw = (nfull & ~3u) + rr;
+			store_b32_nc(bswap32(Ll[jw]), 4u * (g0 + jw), dst_rsrc);
+		}
+	} else {
+		__amdgpu_buffer_rsrc_t rs;
+		__builtin_memcpy(&rs, &dst_rsrc, sizeof(rs));
+		const uint32_t nquad = nfull >> 2;
+#pragma unroll
+		for (uint32_t i = 0; i < NQ; i++) {
+			const uint32_t p = tid + i * NT;
+			const bool in = p < nquad;
+			const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + (in ? 4u * p : 0u));
+			u32x4 o;
+			o.x = bswap32(wv.x);
+			o.y = bswap32(wv.y);
+			o.z = bswap32(wv.z);
+			o.w = bswap32(wv.w);
+			__builtin_amdgcn_raw_buffer_store_b128(o, rs, in ? (int)(4u * (g0 + 4u * p)) : INT32_MIN, 0, 0);
+		}
+		const uint32_t rr = (tid - nquad) & (NT - 1u);
+		const bool part = rr < (nfull & 3u);
+		const uint32_t jw = part ? (nfull & ~3u) + rr : 0u;
+		__builtin_amdgcn_raw_buffer_store_b32(bswap32(Ll[jw]), rs, part ? (int)(4u * (g0 + jw)) : INT32_MIN, 0, 0);
 	}
 	st.carry = (end & 31u) ? __builtin_amdgcn_readfirstlane(Ll[nfull]) : 0u;
 	st.used_prev = nfull + 1u;
@@ -1010,9 +1091,11 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 			uint32_t *const img = (cc & 1u) ? img1 : img0;
 			uint32_t *const imgo = (cc & 1u) ? img0 : img1;
 			if (prim)
-				cw_chunk<ENC_P, RICE_P>(st, img, imgo, s_wsum, cc & 1u, T, mp, oq, cp, fast_p, tab_p, dst_rsrc);
+				cw_chunk<ENC_P, RICE_P, CW_THREADS, CW_NQ>(st, img, imgo, s_wsum, cc & 1u, T, mp, oq, cp, fast_p,
+									    tab_p, dst_rsrc);
 			else
-				cw_chunk<ENC_S, RICE_S>(st, img, imgo, s_wsum, cc & 1u, T, mp, oq, cs, fast_s, tab_s, dst_rsrc);
+				cw_chunk<ENC_S, RICE_S, CW_THREADS, CW_NQ>(st, img, imgo, s_wsum, cc & 1u, T, mp, oq, cs, fast_s,
+									    tab_s, dst_rsrc);
 		}
 		const uint32_t size = ((st.P + 7u) >> 3) + (a.checksum ? 4u : 0u);
 		const uint64_t id = a.ids ? a.ids[f] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)acq * a.id_astep;
