@@ -740,10 +740,9 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 //   * two barriers per chunk: wave totals (B1), packed image (B2).
 // ---------------------------------------------------------------------
 #define CW_THREADS 1024u
-// the context walk's stores per thread and chunk (cw_chunk NQ; two images of
-// at most 150 KiB, ctx_walk_words, hold < 4.7 quads per thread, so 5 would
-// do): 0, the uncounted asm stores, because 5 counted ones took the kernel to
-// 128 VGPRs with scratch spills
+// the context walk's counted stores per thread and chunk (cw_chunk NQ): 0,
+// all uncounted.  The kernel sits at 128 VGPRs; counted stores (2 per thread,
+// or 5, enough for any chunk) spilled to scratch
 #ifndef CW_NQ
 #define CW_NQ 0u
 #endif
@@ -813,7 +812,8 @@ struct CwState {
 // (dropped), as compiler builtins: the compiler then counts them, and its
 // wait for a prefetch issued before them lets them stay in flight (with NQ =
 // 0 that wait, vmcnt(n) for the n loads it knows of, also waited for the
-// uncounted stores, which are younger).  Needs NQ * NT quads >= any chunk's.
+// uncounted stores, which are younger).  Quads past NQ per thread (chunks of
+// long codes) go out uncounted, as with NQ = 0.
 template <int ENC, bool RICE, uint32_t NT = CW_THREADS, uint32_t NQ = 0u>
 __device__ __forceinline__ void cw_chunk(CwState &st, uint32_t *img, uint32_t *imgo, uint32_t (*s_wsum)[NT / 64u],
 					 uint32_t par, uint32_t T, const uint32_t (&mp)[EPT / 2],
@@ -876,6 +876,17 @@ __device__ __forceinline__ void cw_chunk(CwState &st, uint32_t *img, uint32_t *i
 		const bool part = rr < (nfull & 3u);
 		const uint32_t jw = part ? (nfull & ~3u) + rr : 0u;
 		__builtin_amdgcn_raw_buffer_store_b32(bswap32(Ll[jw]), rs, part ? (int)(4u * (g0 + jw)) : INT32_MIN, 0, 0);
+		// a chunk longer than NQ quads per thread (long codes): the rest
+		// uncounted, as with NQ = 0
+		for (uint32_t p = tid + NQ * NT; p < nquad; p += NT) {
+			const u32x4 wv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + 4u * p);
+			u32x4 o;
+			o.x = bswap32(wv.x);
+			o.y = bswap32(wv.y);
+			o.z = bswap32(wv.z);
+			o.w = bswap32(wv.w);
+			store_b128_nc(o, 4u * (g0 + 4u * p), dst_rsrc);
+		}
 	}
 	st.carry = (end & 31u) ? __builtin_amdgcn_readfirstlane(Ll[nfull]) : 0u;
 	st.used_prev = nfull + 1u;
