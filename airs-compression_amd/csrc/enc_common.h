@@ -487,6 +487,7 @@ struct WArgs {
 	uint32_t fb, raw_size; // uncompressed fallback on the chip (walk_ctx_kernel, airs_walk)
 	uint32_t ticket_base;  // walk_kernel: ticket[AIRS_WALK_TICKET] before the launch
 	uint32_t direct;       // walk_kernel: the whole grid is resident, logical index = block index
+	uint32_t cus;          // walk_kernel: compute units of the device (direct launches: issue priority)
 	uint8_t *draws;        // identifier draws per frame (fb)
 	uint8_t *seq_out;      // sequence number per context after the walk (fb)
 	uint32_t dbg;    // ablation builds: AIRS_DBG switches (0 in production)

@@ -308,6 +308,26 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		__syncthreads();
 		lb = __builtin_amdgcn_readfirstlane(s_ctl[3]);
 	}
+	// Dispatch generation (direct launches): the CUs take the grid one
+	// workgroup each per generation, so block b is its CU's (b / CUs)-th.  At
+	// equal priority the oldest waves issue first: the CU's first workgroup
+	// finished its walk in 44 us and its fourth in 62 (cfg5s8), the CU nearly
+	// empty at the end; a fixed priority by generation only inverts that.  The
+	// data waves rotate their priority by step and generation instead (below).
+	const uint32_t gen = (a.direct && a.cus) ? blockIdx.x / a.cus : 0u;
+	auto rotate_prio = [&](uint32_t acq) {
+		if (!(a.direct && a.cus))
+			return;
+		const uint32_t pr = (acq + gen) & 3u;
+		if (pr == 0u)
+			__builtin_amdgcn_s_setprio(0);
+		else if (pr == 1u)
+			__builtin_amdgcn_s_setprio(1);
+		else if (pr == 2u)
+			__builtin_amdgcn_s_setprio(2);
+		else
+			__builtin_amdgcn_s_setprio(3);
+	};
 	const uint32_t c = lb / a.spf, j = lb - c * a.spf;
 	const bool is_first = j == 0u, is_last = j + 1u == a.spf;
 	const uint32_t n = a.n;
@@ -415,6 +435,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 			const bool prim = sq == 0u || sq > a.iters; // cmp.c:228-248
 			if (have)
 				sq = prim ? 1u : sq + 1u;
+			rotate_prio(acq);
 			uint32_t *const img = img_at(acq);
 			uint32_t *const imgp = img_at(acq + NIMG - LAG); // acquisition acq - LAG
 			uint32_t mp[E / 2], oq[E / 2];
@@ -1393,6 +1414,9 @@ static int walk_go(K kern, const WArgs &k, size_t lds, hipStream_t s)
 		per_cu = 0;
 	WArgs kk = k;
 	kk.direct = (cus > 0 && per_cu > 0 && (uint64_t)grid <= (uint64_t)per_cu * (uint64_t)cus) ? 1u : 0u;
+	kk.cus = cus > 0 ? (uint32_t)cus : 0u;
+	if (const char *e = getenv("AIRS_WALK_PRIO")) // A/B: 0 leaves every workgroup at priority 0
+		kk.cus = atoi(e) ? kk.cus : 0u;
 	if (const char *e = getenv("AIRS_WALK_TICKET")) // tests: 1 forces the ticket
 		kk.direct = atoi(e) ? 0u : kk.direct;
 	hipLaunchKernelGGL(kern, dim3(grid), dim3(320), lds, s, kk);

@@ -80,6 +80,12 @@ res = dict(
         step_total=pct(rel[:, 1:, 0] - rel[:, :-1, 0], 90),
     ),
     wait_B2_by_segment_us=[med((rel[:, :, 3] - rel[:, :, 2])[j == s]) for s in range(spf)],
+    # where the slow workgroups are: lifetime (end - start) by segment index,
+    # by stream, and by XCD (slot 7: HW_ID << 32 | XCC_ID)
+    life_by_segment_us=[med((end - start)[j == s]) for s in range(spf)],
+    life_by_stream_us=[med((end - start)[np.arange(nb) // spf == q]) for q in range(nb // spf)],
+    end_by_stream_us=[float(us((end[np.arange(nb) // spf == q]).max())) for q in range(nb // spf)],
+    life_by_xcd_us=[med((end - start)[(ts[:, 0, 7] & 0xF) == x]) for x in range(8)],
 )
 with open(out, "w") as f:
     json.dump(res, f, indent=1)
