@@ -263,7 +263,7 @@ arena_kernel(KArgs a)
 					const uint32_t v = half16(wv, h) + 1u;
 					// bin + 1016 = the top 12 bits of the float v
 					uint32_t ha;
-					asm("v_bfe_u32 %0, %1, 20, 12\n\tv_lshl_add_u32 %0, %0, 7, %2"
+					asm("v_lshrrev_b32 %0, 20, %1\n\tv_lshl_add_u32 %0, %0, 7, %2"
 					    : "=&v"(ha)
 					    : "v"(__float_as_uint((float)v)), "v"(hbase));
 					__hip_atomic_fetch_add(reinterpret_cast<lds_u32 *>((uintptr_t)ha), 1u, __ATOMIC_RELAXED,

@@ -366,7 +366,7 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 		__shared__ uint32_t s_kt[EWG / 64][16];
 		uint32_t *const H = L_dyn;
 		// this lane's counter of bin b is at byte hbase + 256 (b + 1016): the
-		// bin's offset comes from the float bits with one bit-field extract
+		// bin's offset comes from the float bits with one (full-rate) shift
 		// and one shift-add (32-bit LDS address arithmetic wraps)
 		const uint32_t hbase = (uint32_t)(uintptr_t)H + 4u * lane - 1016u * 256u;
 		__syncthreads(); // the images are zeroed
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 						const uint32_t v = half16(wv, h) + 1u;
 						// (as asm: the compiler turns the pair into shift, and, add)
 						uint32_t ha;
-						asm("v_bfe_u32 %0, %1, 20, 12\n\tv_lshl_add_u32 %0, %0, 8, %2"
+						asm("v_lshrrev_b32 %0, 20, %1\n\tv_lshl_add_u32 %0, %0, 8, %2"
 						    : "=&v"(ha)
 						    : "v"(__float_as_uint((float)v)), "v"(hbase));
 						lds_u32 *hp = reinterpret_cast<lds_u32 *>((uintptr_t)ha);

@@ -1261,7 +1261,7 @@ __global__ __launch_bounds__(1024) void frame_auto_kernel(KArgs a)
 				for (uint32_t h = 0; h < 2; h++) {
 					const uint32_t v = half16(wv, h) + 1u;
 					uint32_t ha;
-					asm("v_bfe_u32 %0, %1, 20, 12\n\tv_lshl_add_u32 %0, %0, 8, %2"
+					asm("v_lshrrev_b32 %0, 20, %1\n\tv_lshl_add_u32 %0, %0, 8, %2"
 					    : "=&v"(ha)
 					    : "v"(__float_as_uint((float)v)), "v"(hbase));
 					__hip_atomic_fetch_add(reinterpret_cast<lds_u32 *>((uintptr_t)ha), 1u, __ATOMIC_RELAXED,
