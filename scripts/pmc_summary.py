@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import rocpd_summary  # noqa: E402
 
 SAMPLES = {"cfg2": 64 << 20, "cfg2s": 64 << 20, "cfg3": 64 << 20, "cfg4": 64 << 20,
-           "cfg5": 256 << 20, "cfg5fb": 256 << 20}
+           "cfg5": 256 << 20, "cfg5fb": 256 << 20, "cfg5s8": 32 << 20}
 
 
 def main():
@@ -42,6 +42,14 @@ def main():
                 for key in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
                     if key in c:
                         r[key + "/WAVE_CYCLES"] = round(c[key] / wc, 3)
+            ga = c.get("GRBM_GUI_ACTIVE")
+            if ga:
+                # SIMD-cycles = GUI_ACTIVE / 8 XCDs x 1024 SIMDs; SQ_* wave counters in quad-cycles
+                simd_cycles = ga / 8.0 * 1024.0
+                if "SQ_ACTIVE_INST_VALU" in c:
+                    r["valu_busy"] = round(c["SQ_ACTIVE_INST_VALU"] * 4 / simd_cycles, 3)
+                if wc:
+                    r["resident_waves_per_simd"] = round(wc * 4 / simd_cycles, 3)
             kd = kern.get(kn)
             if kd:
                 r["avg_us"] = kd["avg_us"]
@@ -49,13 +57,14 @@ def main():
             out.setdefault(wl, {})[kn[:80]] = r
         # per-sample figures for the dominant encode kernel (most VALU; the
         # bench's input synthesis is not part of the path)
-        enc = {k: v for k, v in out.get(wl, {}).items() if "encode_kernel" in k or "walk_kernel" in k}
+        enc = {k: v for k, v in out.get(wl, {}).items()
+               if "encode_kernel" in k or "walk_kernel" in k or "walk_ctx_kernel" in k}
         dom = max(enc.items(), key=lambda kv: kv[1].get("SQ_INSTS_VALU", 0), default=None)
         if dom:
             kn, r = dom
             n = SAMPLES.get(wl)
-            if wl.startswith("cfg5") and "walk_kernel" not in kn:
-                n = n // 16  # per-step launches: one acquisition of the 256 streams
+            if wl.startswith("cfg5") and "encode_kernel" in kn:
+                n = n // 16  # per-step launches: one acquisition of the streams
             per = {k: round(r[k] * 64 / n, 3) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS",
                                                           "SQ_INSTS_SMEM") if k in r}
             out[wl]["_per_sample_dominant"] = dict(kernel=kn, samples_per_launch=n,
