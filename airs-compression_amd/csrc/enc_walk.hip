@@ -53,6 +53,10 @@ namespace airs {
 #define AIRS_WALK_LAG 1u
 #endif
 #define AIRS_WALK_NIMG (AIRS_WALK_LAG + 2u)
+// counted output stores per data thread and step of the segment walk
+#ifndef AIRS_WALK_NQ
+#define AIRS_WALK_NQ 1u
+#endif
 
 // table entry idx of a pass: {T, len}; see the header comment
 template <int ENC>
@@ -428,7 +432,11 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		__builtin_amdgcn_s_waitcnt(0x0F70);
 		uint32_t A1 = 0u, A2 = 0u, A3 = 0u; // the bit totals of acquisitions acq - 1, acq - 2, acq - 3
 		// quads of one image per data thread, at most (48-bit codewords)
-		constexpr uint32_t NQ = (SEGW * 48u / 32u / 4u + 2u + ND - 1u) / ND;
+		// counted 16-byte stores per thread and step: one covers segments of up
+		// to 16 bits per sample (cfg5's are ~7); the quads past it (noisy
+		// segments) go out uncounted (the fixed-count form with room for 48-bit
+		// codes cost ~6 VALU instructions per sample at 8 samples per lane)
+		constexpr uint32_t NQ = AIRS_WALK_NQ;
 		for (uint32_t acq = 0; acq < a.fpc + LAG; acq++) {
 			const bool have = acq < a.fpc, prev = acq >= LAG;
 			const uint32_t f = c * a.fpc + acq;
@@ -564,6 +572,21 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 				const uint32_t v = __builtin_amdgcn_alignbit(hi, Ll[jw], r);
 				__builtin_amdgcn_raw_buffer_store_b32(bswap32(v), dst_rsrc, part ? (int)(4u * (g0 + jw)) : INT32_MIN, 0,
 								      0);
+				if (nquad > NQ * ND) { // the rest, uncounted (walk_ctx_kernel's stores)
+					const u32x4 rs4 = rsrc_words(fdst, a.cap & ~3u);
+					for (uint32_t p = tid + NQ * ND; p < nquad; p += ND) {
+						const uint32_t jq = 4u * p;
+						const u32x4 wv =
+							*reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + jq);
+						const uint32_t hq = Ll[jq - 1u];
+						u32x4 o;
+						o.x = bswap32(__builtin_amdgcn_alignbit(hq, wv.x, r));
+						o.y = bswap32(__builtin_amdgcn_alignbit(wv.x, wv.y, r));
+						o.z = bswap32(__builtin_amdgcn_alignbit(wv.y, wv.z, r));
+						o.w = bswap32(__builtin_amdgcn_alignbit(wv.z, wv.w, r));
+						store_b128_nc(o, 4u * (g0 + jq), rs4);
+					}
+				}
 				if (prev && wid == 0u)
 					wstamp(a, acq - LAG, 4u);
 			}
