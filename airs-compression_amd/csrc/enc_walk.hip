@@ -46,6 +46,11 @@ namespace airs {
 
 // rows of the code tables in LDS (one table per pass)
 #define WTAB 48u
+// walk_lengths' GOLOMB_MULTI path for waves without an escape (packed, no
+// table reads); 0 for A/B builds
+#ifndef AIRS_MULTI_FAST
+#define AIRS_MULTI_FAST 1
+#endif
 // The segment walk stores acquisition a in step a + LAG, and keeps LAG + 2
 // LDS images: acquisition a + 1 packs into the image stored two steps
 // earlier, so no barrier clears the one just stored
@@ -147,7 +152,10 @@ __device__ __forceinline__ void store_b32_nc(uint32_t v, uint32_t byte_off, u32x
 
 // one pass's residual-independent coding: table offsets (8 idx per sample,
 // 16-bit halves of oq[]), lengths total of the lane; returns the lane's bits
-template <int ENC, bool RICE, int NP>
+// MF: the GOLOMB_MULTI paths for escape-free waves below (the segment walk;
+// the context walk, at 128 VGPRs, measured slower with them: 392-405 against
+// 373-379 us on cfg5)
+template <int ENC, bool RICE, int NP, bool MF = false>
 __device__ __forceinline__ uint32_t walk_lengths(const uint32_t (&mp)[NP], uint32_t (&oq)[NP], const Coder &cd,
 						 bool fast, const char *tab)
 {
@@ -165,6 +173,27 @@ __device__ __forceinline__ uint32_t walk_lengths(const uint32_t (&mp)[NP], uint3
 	}
 	if (ENC == ENC_MULTI && RICE) {
 		const uint32_t om1 = cd.outlier - 1u;
+		// no escape anywhere in the wave (wave-uniform test): every code is
+		// unary q = m >> k, then k bits, length q + k + 1; the offsets and
+		// the lengths' sum come from packed shifts and adds, no table reads
+		// (the sums of NP q per half stay below 2^16: (om1 >> k) NP < 2^16)
+		if constexpr (MF) {
+			u16x2 mx = (u16x2)(0);
+#pragma unroll
+			for (uint32_t j = 0; j < NP; j++)
+				mx = __builtin_elementwise_max(mx, pk(mp[j]));
+			const uint32_t mxu = unpk(mx), mxs = max(mxu & 0xFFFFu, mxu >> 16);
+			if (MF && AIRS_MULTI_FAST && (om1 >> cd.k) * NP < 65536u && __ballot(mxs > om1) == 0ull) {
+				u16x2 acc = (u16x2)(0);
+#pragma unroll
+				for (uint32_t j = 0; j < NP; j++) {
+					const u16x2 q = pk(mp[j]) >> (u16x2)((unsigned short)cd.k);
+					acc += q;
+					oq[j] = unpk(q << (u16x2)(3));
+				}
+				return 2u * NP * (cd.k + 1u) + (unpk(acc) & 0xFFFFu) + (unpk(acc) >> 16);
+			}
+		}
 #pragma unroll
 		for (uint32_t j = 0; j < NP; j++) {
 			uint32_t o2 = 0u;
@@ -188,7 +217,7 @@ __device__ __forceinline__ uint32_t walk_lengths(const uint32_t (&mp)[NP], uint3
 }
 
 // pack the lane's 2 NP codewords from bit `excl` of the image
-template <int ENC, bool RICE, int NP>
+template <int ENC, bool RICE, int NP, bool MF = false>
 __device__ __forceinline__ void walk_pack(uint32_t *img, uint32_t excl, const uint32_t (&mp)[NP],
 					  const uint32_t (&oq)[NP], const Coder &cd, bool fast, const char *tab)
 {
@@ -238,6 +267,24 @@ __device__ __forceinline__ void walk_pack(uint32_t *img, uint32_t excl, const ui
 			for (uint32_t i = 0; i < 8u; i++) {
 				const uint32_t j = hb * 8u + i;
 				te[i] = *reinterpret_cast<const uint2 *>(tab + half16(oq[j >> 1], j & 1u));
+			}
+			// every pair of the batch fits one put (the wave's short codes, as
+			// in the ZERO path): half the puts
+			uint32_t mxl = 0u;
+			if constexpr (MF) {
+#pragma unroll
+				for (uint32_t i = 0; i < 8u; i += 2)
+					mxl = max(mxl, te[i].y + te[i + 1].y);
+			}
+			if (MF && AIRS_MULTI_FAST && __ballot(mxl > 32u) == 0ull) {
+#pragma unroll
+				for (uint32_t i = 0; i < 8u; i += 2) {
+					const uint32_t j = hb * 8u + i;
+					const uint32_t cwa = (mp[j >> 1] & 0xFFFFu) + te[i].x;
+					const uint32_t cwb = (mp[j >> 1] >> 16) + te[i + 1].x;
+					pk1.put((cwa << te[i + 1].y) | cwb, te[i].y + te[i + 1].y);
+				}
+				continue;
 			}
 #pragma unroll
 			for (uint32_t i = 0; i < 8u; i++) {
@@ -485,7 +532,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 						mp[q] = ENC_P == ENC_RAW ? u : zigzag_pk(u);
 						mdl[q] = w[q]; // cmp.c:305-306: the model takes the samples
 					}
-					T = walk_lengths<ENC_P, RICE_P>(mp, oq, cp, fast_p, tab_p);
+					T = walk_lengths<ENC_P, RICE_P, E / 2, true>(mp, oq, cp, fast_p, tab_p);
 				} else {
 					const int32_t r1 = 16 - (int32_t)a.model_rate;
 #pragma unroll
@@ -494,7 +541,7 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 						mp[q] = ENC_S == ENC_RAW ? u : zigzag_pk(u);
 						mdl[q] = model_update_zx(w[q], mdl[q], r1); // cmp.c:132-142
 					}
-					T = walk_lengths<ENC_S, RICE_S>(mp, oq, cs, fast_s, tab_s);
+					T = walk_lengths<ENC_S, RICE_S, E / 2, true>(mp, oq, cs, fast_s, tab_s);
 				}
 #pragma unroll
 				for (uint32_t q = 0; q < E / 2; q++)
@@ -519,9 +566,9 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 				excl += wpre;
 				// ---- pack into this acquisition's image -----------------------------
 				if (prim)
-					walk_pack<ENC_P, RICE_P>(img, excl, mp, oq, cp, fast_p, tab_p);
+					walk_pack<ENC_P, RICE_P, E / 2, true>(img, excl, mp, oq, cp, fast_p, tab_p);
 				else
-					walk_pack<ENC_S, RICE_S>(img, excl, mp, oq, cs, fast_s, tab_s);
+					walk_pack<ENC_S, RICE_S, E / 2, true>(img, excl, mp, oq, cs, fast_s, tab_s);
 				if (wid == DW - 1u && !is_last) {
 					// the segment's last 32 bits (wave 3's own lanes wrote them) for
 					// the successor's first word (read by it one step later)
