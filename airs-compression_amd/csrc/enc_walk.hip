@@ -59,6 +59,11 @@ namespace airs {
 #endif
 #define AIRS_WALK_NIMG (AIRS_WALK_LAG + 2u)
 // counted output stores per data thread and step of the segment walk
+// frames per context up to which the segment walk writes its frame epilogues
+// after the walk (4 LDS words per frame); 0: in the step loop
+#ifndef AIRS_WALK_EPI_MAX
+#define AIRS_WALK_EPI_MAX 64u
+#endif
 #ifndef AIRS_WALK_NQ
 #define AIRS_WALK_NQ 1u
 #endif
@@ -662,6 +667,46 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 		// its predecessor tail, issued at the end of the step before, evaluated
 		// after B1
 		uint64_t gv0 = 0ull, tv0 = 0ull;
+		// The frame epilogue's stores (header words, final bytes, checksum,
+		// status: partial cache lines) cost the last segment's control wave
+		// ~5 us per cfg5s8 launch inside the step loop (the compiler's waits
+		// for the next look-back loads covered them).  With at most
+		// AIRS_WALK_EPI_MAX frames per context they are kept in LDS (four words
+		// per frame) and written after the walk, one frame per lane.
+		const bool defer = a.fpc <= AIRS_WALK_EPI_MAX;
+		uint32_t *const epi = L_img + 4u + NIMG * (a.img_words + 4u);
+		// frame ai of this context: payload bytes, final word (written when
+		// nbytes > 0) at byte offset fwoff, meta = header sequence number |
+		// primary << 8 | 22-byte header << 9 | nbytes << 16
+		auto frame_epilogue = [&](uint32_t ai, uint32_t payload_bytes, uint32_t v, uint32_t fwoff, uint32_t meta) {
+			const uint32_t fp = c * a.fpc + ai;
+			uint8_t *fdst = a.dst + (uint64_t)fp * a.dst_stride;
+			const uint32_t nbytes = meta >> 16;
+			for (uint32_t b = 0; b < nbytes; b++)
+				if (fwoff + b < a.cap)
+					fdst[fwoff + b] = (uint8_t)(v >> (24u - 8u * b));
+			const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
+			if (a.checksum) {
+				const uint32_t ck = a.checksums[fp];
+				for (uint32_t b = 0; b < 4u; b++)
+					if (payload_bytes + b < a.cap)
+						fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
+			}
+			const uint64_t id = a.ids ? a.ids[fp] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)ai * a.id_astep;
+			const uint32_t hs = meta & 0xFFu;
+			uint32_t h[5];
+			if (meta & 0x100u)
+				header_words(h, size, 2u * n, id, hs, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
+					     ENC_P == ENC_RAW ? 0u : cp.g, ENC_P == ENC_RAW ? 0u : cp.outlier);
+			else
+				header_words(h, size, 2u * n, id, hs, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S, a.model_rate,
+					     ENC_S == ENC_RAW ? 0u : cs.g, ENC_S == ENC_RAW ? 0u : cs.outlier);
+			const uint32_t hwords = (meta & 0x200u) ? 5u : 4u;
+			for (uint32_t wq = 0; wq < hwords; wq++)
+				if (4u * wq + 4u <= a.cap)
+					*reinterpret_cast<uint32_t *>(fdst + 4u * wq) = bswap32(h[wq]);
+			a.status[fp] = size > a.cap ? ERRV(E_DST_TOO_SMALL) : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
+		};
 		for (uint32_t acq = 0; acq < a.fpc + LAG; acq++) {
 			const bool have = acq < a.fpc, prev = acq >= LAG;
 			const uint32_t f = c * a.fpc + acq;
@@ -746,45 +791,29 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 			}
 			lds_barrier(); // B2
 			if (prev && is_last && lane == 0u) {
-				// ---- frame epilogue (cmp.c:314-334) ---------------------------------
-				const uint32_t fp = f - LAG;
+				// ---- frame epilogue (cmp.c:314-334): the final word, kept for
+				// the end of the walk (or written now, frame_epilogue) --------------
 				uint32_t *const imgp = img_at(acq + NIMG - LAG);
 				const uint32_t r = P & 31u, g0 = P >> 5;
 				const uint32_t endbit = P + A_st;
 				const uint32_t J = ((endbit - 1u) >> 5) - g0; // last word touched
 				const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
-				uint8_t *fdst = a.dst + (uint64_t)fp * a.dst_stride;
+				uint32_t v = 0u, nbytes = 0u;
 				if (nfull == J) { // zero-padded final bytes (bitstream_flush)
 					const uint32_t hi = J ? imgp[J - 1u] : pred;
-					const uint32_t v = __builtin_amdgcn_alignbit(hi, imgp[J], r);
-					const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
-					for (uint32_t b = 0; b < nbytes; b++)
-						if (4u * (g0 + J) + b < a.cap)
-							fdst[4u * (g0 + J) + b] = (uint8_t)(v >> (24u - 8u * b));
+					v = __builtin_amdgcn_alignbit(hi, imgp[J], r);
+					nbytes = ((endbit & 31u) + 7u) >> 3;
 				}
-				const uint32_t payload_bytes = (endbit + 7u) >> 3;
-				const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
-				if (a.checksum) {
-					const uint32_t ck = a.checksums[fp];
-					for (uint32_t b = 0; b < 4u; b++)
-						if (payload_bytes + b < a.cap)
-							fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
+				const uint32_t meta = hseq_st | (prim_st ? 0x100u : 0u) | (HB_st == 176u ? 0x200u : 0u) | nbytes << 16;
+				if (defer) {
+					uint32_t *const rec = epi + 4u * (acq - LAG);
+					rec[0] = (endbit + 7u) >> 3;
+					rec[1] = v;
+					rec[2] = 4u * (g0 + J);
+					rec[3] = meta;
+				} else {
+					frame_epilogue(acq - LAG, (endbit + 7u) >> 3, v, 4u * (g0 + J), meta);
 				}
-				const uint64_t id =
-					a.ids ? a.ids[fp] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)(acq - LAG) * a.id_astep;
-				uint32_t h[5];
-				if (prim_st)
-					header_words(h, size, 2u * n, id, hseq_st, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
-						     ENC_P == ENC_RAW ? 0u : cp.g, ENC_P == ENC_RAW ? 0u : cp.outlier);
-				else
-					header_words(h, size, 2u * n, id, hseq_st, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S,
-						     a.model_rate, ENC_S == ENC_RAW ? 0u : cs.g, ENC_S == ENC_RAW ? 0u : cs.outlier);
-				const uint32_t hwords = HB_st == 176u ? 5u : 4u;
-				for (uint32_t wq = 0; wq < hwords; wq++)
-					if (4u * wq + 4u <= a.cap)
-						*reinterpret_cast<uint32_t *>(fdst + 4u * wq) = bswap32(h[wq]);
-				a.status[fp] = size > a.cap ? ERRV(E_DST_TOO_SMALL)
-							    : size > 0xFFFFFFu ? ERRV(E_HDR_CMP_SIZE_TOO_LARGE) : size;
 			}
 			if (acq + 1u >= LAG && acq + 1u - LAG < a.fpc && !is_first) {
 				// the look-back of acquisition acq + 1 - LAG (next step)
@@ -801,6 +830,13 @@ __global__ __launch_bounds__(320) void walk_kernel(WArgs a)
 			HB1 = HB;
 			hseq1 = hseq;
 			prim1 = prim;
+		}
+		if (defer && is_last) {
+			// the epilogues kept in LDS (written by this wave's lane 0)
+			for (uint32_t ai = lane; ai < a.fpc; ai += 64u) {
+				const uint32_t *const rec = epi + 4u * ai;
+				frame_epilogue(ai, rec[0], rec[1], rec[2], rec[3]);
+			}
 		}
 	}
 	// the model after the last acquisition, to the work buffer (cmp.c:304-311)
@@ -1569,7 +1605,9 @@ bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint
 int walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
 		bool rice_s, hipStream_t s)
 {
-	const size_t lds = (size_t)(AIRS_WALK_NIMG * (k.img_words + 4u) + 4u) * 4u; // walk_kernel's images
+	// walk_kernel's images, then the deferred frame epilogues
+	const size_t lds = (size_t)(AIRS_WALK_NIMG * (k.img_words + 4u) + 4u) * 4u +
+			   (k.fpc <= AIRS_WALK_EPI_MAX ? (size_t)k.fpc * 16u : 0u);
 	if (sample_bytes == 2)
 		return pre_p == PRE_DIFF ? walk_launch_p<2, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
 					 : walk_launch_p<2, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);
