@@ -1186,6 +1186,32 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 	uint32_t sq = seq0;
 	CwState st;
 	st.used_prev = 0u;
+	// Frame epilogues (header words, final bytes, checksum, status: partial
+	// cache lines) of up to AIRS_WALK_EPI_MAX frames are kept in LDS, four
+	// words per frame, and written after the walk (as the segment walk's,
+	// DESIGN.md 3.7): in the loop, the next waits of wave 0 covered them
+	const bool defer = a.fpc <= AIRS_WALK_EPI_MAX;
+	uint32_t *const epi = L_img + 4u + 2u * a.img_words;
+	if (defer && tid < a.fpc)
+		epi[4u * tid + 3u] = 0u; // no epilogue (a fallback frame) until written
+	auto frame_id = [&](uint32_t ai) {
+		return a.ids ? a.ids[c * a.fpc + ai] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)ai * a.id_astep;
+	};
+	// frame ai: total size, end bit, carry word, meta = header sequence number
+	// | primary << 8 | 22-byte header << 9
+	auto frame_epilogue = [&](uint32_t ai, uint32_t size, uint32_t endbit, uint32_t carry, uint32_t meta) {
+		const uint32_t fr = c * a.fpc + ai;
+		const uint64_t id = frame_id(ai);
+		uint32_t h[5];
+		if (meta & 0x100u)
+			header_words(h, size, 2u * n, id, meta & 0xFFu, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
+				     ENC_P == ENC_RAW ? 0u : cp.g, ENC_P == ENC_RAW ? 0u : cp.outlier);
+		else
+			header_words(h, size, 2u * n, id, meta & 0xFFu, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S, a.model_rate,
+				     ENC_S == ENC_RAW ? 0u : cs.g, ENC_S == ENC_RAW ? 0u : cs.outlier);
+		cw_epilogue(a.dst + (uint64_t)fr * a.dst_stride, a.cap, endbit, carry, (meta & 0x200u) ? 176u : 128u,
+			    a.checksum != 0u, a.checksum ? a.checksums[fr] : 0u, h, a.status, nullptr, fr, size);
+	};
 	for (uint32_t acq = 0; acq < a.fpc; acq++) {
 		const uint32_t f = c * a.fpc + acq;
 		const bool prim = sq == 0u || sq > a.iters; // cmp.c:228-248
@@ -1236,7 +1262,6 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 									    tab_s, dst_rsrc);
 		}
 		const uint32_t size = ((st.P + 7u) >> 3) + (a.checksum ? 4u : 0u);
-		const uint64_t id = a.ids ? a.ids[f] : a.id_base + (uint64_t)c * a.id_cstep + (uint64_t)acq * a.id_astep;
 		// the uncompressed fallback (cmp.c:342-393): the attempt ran with the
 		// raw frame size as its capacity (a.cap); a frame that does not fit is
 		// reset and written raw (block-uniform: st.P is)
@@ -1244,18 +1269,28 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 		if (a.draws && tid == 0u) // identifier draws: one per reset (cmp.c:228-231, 371-392)
 			a.draws[f] = (uint8_t)(prim ? (fbk ? 3u : 1u) : (fbk ? 2u : 0u));
 		if (fbk) {
-			cw_fallback<W, CH>(a, f, fdst, id, flip, mdl);
+			cw_fallback<W, CH>(a, f, fdst, frame_id(acq), flip, mdl);
 			sq = 1u; // the fallback frame has sequence number 0, the next 1
 		} else if (tid == 0u) {
-			uint32_t h[5];
-			if (prim)
-				header_words(h, size, 2u * n, id, hseq, PRE_P, a.checksum ? 1u : 0u, ENC_P, 0u,
-					     ENC_P == ENC_RAW ? 0u : cp.g, ENC_P == ENC_RAW ? 0u : cp.outlier);
-			else
-				header_words(h, size, 2u * n, id, hseq, PRE_MODEL, a.checksum ? 1u : 0u, ENC_S, a.model_rate,
-					     ENC_S == ENC_RAW ? 0u : cs.g, ENC_S == ENC_RAW ? 0u : cs.outlier);
-			cw_epilogue(fdst, a.cap, st.P, st.carry, HB, a.checksum != 0u, a.checksum ? a.checksums[f] : 0u, h,
-				    a.status, nullptr, f, size);
+			const uint32_t meta = hseq | (prim ? 0x100u : 0u) | (HB == 176u ? 0x200u : 0u);
+			if (defer) { // written after the walk (see frame_epilogue)
+				uint32_t *const rec = epi + 4u * acq;
+				rec[0] = size;
+				rec[1] = st.P;
+				rec[2] = st.carry;
+				rec[3] = meta | 0x400u;
+			} else {
+				frame_epilogue(acq, size, st.P, st.carry, meta);
+			}
+		}
+	}
+	if (defer && tid < 64u) {
+		// the epilogues kept in LDS (written by thread 0 in the loop; frames
+		// that took the fallback have none)
+		for (uint32_t ai = tid; ai < a.fpc; ai += 64u) {
+			const uint32_t *const rec = epi + 4u * ai;
+			if (rec[3] & 0x400u)
+				frame_epilogue(ai, rec[0], rec[1], rec[2], rec[3]);
 		}
 	}
 	if (a.seq_out && tid == 0u)
@@ -1594,7 +1629,8 @@ bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint
 {
 	if (k.n != 4u * CW_CHUNK)
 		return false;
-	const size_t lds = (size_t)(2u * k.img_words + 4u) * 4u;
+	// walk_ctx_kernel's two images, then the deferred frame epilogues
+	const size_t lds = (size_t)(2u * k.img_words + 4u) * 4u + (k.fpc <= AIRS_WALK_EPI_MAX ? (size_t)k.fpc * 16u : 0u);
 	if (sample_bytes == 2)
 		return pre_p == PRE_DIFF ? walk_ctx_launch_p<2, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
 					 : walk_ctx_launch_p<2, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);
