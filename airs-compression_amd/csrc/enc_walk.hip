@@ -1266,9 +1266,14 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 		// raw frame size as its capacity (a.cap); a frame that does not fit is
 		// reset and written raw (block-uniform: st.P is)
 		const bool fbk = a.fb && size > a.raw_size;
-		if (a.draws && tid == 0u) // identifier draws: one per reset (cmp.c:228-231, 371-392)
-			a.draws[f] = (uint8_t)(prim ? (fbk ? 3u : 1u) : (fbk ? 2u : 0u));
+		// identifier draws: one per reset (cmp.c:228-231, 371-392); with the
+		// deferred epilogues kept in the frame's record (bits 12-13)
+		const uint32_t draws = prim ? (fbk ? 3u : 1u) : (fbk ? 2u : 0u);
+		if (a.draws && tid == 0u && !defer)
+			a.draws[f] = (uint8_t)draws;
 		if (fbk) {
+			if (defer && tid == 0u)
+				epi[4u * acq + 3u] = draws << 12;
 			cw_fallback<W, CH>(a, f, fdst, frame_id(acq), flip, mdl);
 			sq = 1u; // the fallback frame has sequence number 0, the next 1
 		} else if (tid == 0u) {
@@ -1278,7 +1283,7 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 				rec[0] = size;
 				rec[1] = st.P;
 				rec[2] = st.carry;
-				rec[3] = meta | 0x400u;
+				rec[3] = meta | 0x400u | draws << 12;
 			} else {
 				frame_epilogue(acq, size, st.P, st.carry, meta);
 			}
@@ -1289,6 +1294,8 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 		// that took the fallback have none)
 		for (uint32_t ai = tid; ai < a.fpc; ai += 64u) {
 			const uint32_t *const rec = epi + 4u * ai;
+			if (a.draws)
+				a.draws[c * a.fpc + ai] = (uint8_t)((rec[3] >> 12) & 3u);
 			if (rec[3] & 0x400u)
 				frame_epilogue(ai, rec[0], rec[1], rec[2], rec[3]);
 		}

@@ -36,7 +36,7 @@ BUDGETS = {
     # cfg2s: payload-only stream
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb1EEEvNS_5KArgsE": (128, 0),
     # cfg5 / cfg5fb: the context walk (1024-thread workgroups: <= 128 VGPRs)
-    "_ZN4airs15walk_ctx_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi4EEEvNS_5WArgsE": (128, 72),
+    "_ZN4airs15walk_ctx_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi4EEEvNS_5WArgsE": (128, 74),
     # the segment walk, 16 samples per lane and 8 (cfg5s8: grids of fewer than 1024 4096-sample workgroups)
     "_ZN4airs11walk_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi16EEEvNS_5WArgsE": (112, 28),
     "_ZN4airs11walk_kernelILi4ELi1ELi1ELb1ELi2ELb1ELi8EEEvNS_5WArgsE": (80, 26),
