@@ -210,6 +210,25 @@ def test_walk_contexts_at_different_steps(prod, eng, orc):
     assert got == want
 
 
+def test_walk_many_frames_per_context(prod, eng, orc):
+    """More frames per context than the walk keeps deferred epilogues for
+    (AIRS_WALK_EPI_MAX = 64, enc_walk.hip): 70 acquisitions take the in-loop
+    frame epilogue; 64 the deferred one; checksums and non-affine identifiers
+    (contexts at different steps) on both."""
+    rng = np.random.default_rng(17)
+    kind, n, nctx = "i16", 4096, 2
+    p = P(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16, secondary_iterations=5,
+          secondary_preprocessing=3, secondary_encoder_type=2, secondary_encoder_param=8,
+          secondary_encoder_outlier=107, model_rate=11, checksum_enabled=1)
+    params = [p] * nctx
+    cap = 26 + 6 * n
+    calls = [(1, 2, 1, make_frames(kind, n, 1, rng)), (70, make_frames(kind, n, nctx * 70, rng)),
+             (64, make_frames(kind, n, nctx * 64, rng))]
+    want = run_host(orc, params, kind, n, nctx, calls, cap)
+    got = run_gpu(prod, eng, params, kind, n, nctx, calls, cap)
+    assert got == want
+
+
 def test_walk_cfg5_shape(prod, eng, orc, orc_ext):
     """BASELINE config 5's parameters and sample type (DIFF + ZERO g=16, then
     MODEL + MULTI g=8 o=107 rate 11, 15 secondaries) on 16 acquisitions of
