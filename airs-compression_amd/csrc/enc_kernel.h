@@ -1115,10 +1115,21 @@ __global__ __launch_bounds__(EWG) AIRS_EWPE_ATTR void encode_kernel(KArgs a)
 			     PRE == PRE_MODEL ? a.model_rate : 0u, ENC == ENC_RAW ? 0u : gpar,
 			     ENC == ENC_RAW ? 0u : cd.outlier);
 		const uint32_t hwords = EXT_HDR ? 5u : 4u;
+		if (((uintptr_t)fdst & 7u) == 0u && cap >= 4u * hwords) {
+			// three stores instead of five (8-byte aligned frame): the partial
+			// line shared with the frame's first segment; an ablation without
+			// the header measured 1-2 us faster on cfg3/cfg4, this form the same
+			// 
+			*reinterpret_cast<uint2 *>(fdst) = make_uint2(bswap32(h[0]), bswap32(h[1]));
+			*reinterpret_cast<uint2 *>(fdst + 8) = make_uint2(bswap32(h[2]), bswap32(h[3]));
+			if (hwords == 5u)
+				*reinterpret_cast<uint32_t *>(fdst + 16) = bswap32(h[4]);
+		} else {
 #pragma unroll
-		for (uint32_t w = 0; w < 5u; w++)
-			if (w < hwords && 4u * w + 4u <= cap)
-				*reinterpret_cast<uint32_t *>(fdst + 4u * w) = bswap32(h[w]);
+			for (uint32_t w = 0; w < 5u; w++)
+				if (w < hwords && 4u * w + 4u <= cap)
+					*reinterpret_cast<uint32_t *>(fdst + 4u * w) = bswap32(h[w]);
+		}
 		uint32_t st = size;
 		if (size > cap)
 			st = ERRV(E_DST_TOO_SMALL);
