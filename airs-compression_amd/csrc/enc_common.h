@@ -511,6 +511,9 @@ uint32_t walk_seg_samples(bool half);
 // the arena kernel (enc_arena.hip): 16-bit NONE/DIFF GOLOMB_ZERO g = 2^k <=
 // 2048, no model, whole segments; k.img_words = arena_words()
 bool arena_encode(const KArgs &k, uint32_t pre, bool stream, uint32_t grid, hipStream_t s);
+// the Rice/ZERO frame kernel (enc_rice.hip): 16-bit NONE/DIFF, one g = 2^k
+// (k <= 7), no model, whole 16 Ki-sample segments; false: not eligible
+bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s);
 uint32_t arena_words();
 bool arena_enabled();
 // AUTO (fused per-frame Rice k) launches of frames of whole 16 Ki-sample

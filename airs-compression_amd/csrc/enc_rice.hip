@@ -1,0 +1,592 @@
+// enc_rice.hip -- the Rice/ZERO frame kernel for 16-bit samples (gfx950):
+// the encode hot path of BASELINE configs[1] and configs[3] (cfg2, cfg4).
+//
+// Same output as encode_kernel (enc_kernel.h), bit for bit: reference
+// lib/compress/cmp.c:296-312 (per-sample loop), NONE/DIFF residuals
+// preprocess.c:268-300, ZigZag encoder.c:274-286, Golomb ZERO with g = 2^k
+// encoder.c:327-351 (zero escape :340-346), big-endian bit packing
+// bitstream_writer.h:124-158 with its flush :205-227, header header.c:24-67,
+// checksum header.c:137-163.  Eligible: 16-bit samples, NONE or DIFF,
+// GOLOMB_ZERO with g = 2^k, k <= RICE_KMAX, no model, whole 16 Ki-sample
+// segments, 16-byte aligned frames.
+//
+// What differs from encode_kernel is how much of the chip a segment holds
+// while it waits:
+//   * phase 1 turns every sample pair into its final codeword pair V (one
+//     32-bit register: the two codewords back to back) and its length L
+//     (four lengths per register), instead of keeping the mapped values AND
+//     the code-table offsets: 40 registers per lane for the segment's 64
+//     samples instead of 64, so five workgroups (20 waves) fit a CU instead
+//     of four.  The table lookups move into phase 1, where they overlap the
+//     sample loads of the other workgroups; the packer reads no LDS at all;
+//   * the segment is packed back to back into ONE arena sized for a
+//     compressed segment (~15.7 bits per sample; a segment that does not
+//     fit is packed and stored chunk by chunk), so there is no image
+//     rotation: three barriers per segment (encode_kernel: seven);
+//   * the look-back is evaluated once the whole segment is packed, so its
+//     predecessors published their aggregates long before (no retries).
+// A pair whose two codewords exceed 32 bits (two zero escapes, or one
+// escape next to a long code) keeps its mapped values in V; the packer
+// re-codes it from the table in a wave-uniform slow step.
+//
+// Look-back granules, frame-interleaved dispatch, the tail granule and the
+// bounded spins are those of encode_kernel.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "enc_common.h"
+
+namespace airs {
+
+#ifndef AIRS_RICE_WPE // workgroups (= waves per SIMD) per CU the kernel is built for
+#define AIRS_RICE_WPE 5
+#endif
+#define RICE_KMAX 7u       // largest k this kernel takes (pairs of typical codes fit 32 bits)
+constexpr uint32_t RCH = 4u;                 // chunks of AIRS_SEG samples per segment
+constexpr uint32_t RSEGN = RCH * AIRS_SEG;   // 16384 samples per segment
+constexpr uint32_t RGUARD = 4u;              // words before the arena (a lane's first put ORs zeros there)
+constexpr uint32_t RSTATIC = 512u;           // static LDS of the kernel, rounded up
+static_assert(EPT == 16u, "lane t owns samples [16t, 16t+16) of each chunk");
+
+// arena words (guard included) for AIRS_RICE_WPE workgroups per CU
+__host__ __device__ constexpr uint32_t rice_arena_words()
+{
+	return ((160u * 1024u / AIRS_RICE_WPE - RSTATIC) / 4u) & ~3u;
+}
+
+// the four words of a lane's chunk: lengths of pairs 4h .. 4h+3, a byte each
+__device__ __forceinline__ uint32_t len_byte(const uint32_t (&lp)[2], uint32_t j)
+{
+	const uint32_t w = lp[j >> 2], b = j & 3u;
+	return b == 0u ? (w & 0xFFu) : b == 3u ? (w >> 24) : ((w >> (8u * b)) & 0xFFu);
+}
+
+// (codeword, length) of one mapped value from the table (slow steps only)
+__device__ __forceinline__ uint2 rice_code(uint32_t m, uint32_t k, const uint2 *tab)
+{
+	const uint32_t q = (m + 1u) >> k;
+	const uint2 e = tab[q < 17u ? q : 17u];
+	return make_uint2(m + e.x, e.y);
+}
+
+// Bit packer of one lane into the arena (as enc_common.h Packer): nb is the
+// bit position in the LDS address space less 32, acc the last bits.
+struct RPack {
+	uint64_t acc;
+	uint32_t nb;
+	__device__ __forceinline__ void init(uint32_t bitaddr)
+	{
+		acc = 0u;
+		nb = bitaddr - 32u;
+	}
+	__device__ __forceinline__ void put(uint32_t v, uint32_t len) // len <= 32, v < 2^len
+	{
+		acc = (acc << len) | v;
+		nb += len;
+		lds_u32 *w = reinterpret_cast<lds_u32 *>((uintptr_t)((nb >> 3) & ~3u));
+		__hip_atomic_fetch_or(w, __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, nb),
+				      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+	}
+	__device__ __forceinline__ void flush()
+	{
+		if (nb & 31u) {
+			lds_u32 *w = reinterpret_cast<lds_u32 *>((uintptr_t)(((nb >> 3) & ~3u) + 4u));
+			__hip_atomic_fetch_or(w, (uint32_t)acc << (32u - (nb & 31u)), __ATOMIC_RELAXED,
+					      __HIP_MEMORY_SCOPE_WORKGROUP);
+		}
+	}
+};
+
+// Pack one lane's 8 pairs of a chunk.  Pairs of more than 32 bits hold their
+// mapped values in V (the two halves) and are re-coded here; the test is one
+// ballot per chunk, then one per pair inside chunks that have such a pair.
+__device__ __forceinline__ void pack_chunk(RPack &p, const uint32_t (&V)[8], const uint32_t (&lp)[2], uint32_t k,
+					   const uint2 *tab)
+{
+	const uint32_t ov = ((lp[0] + 0x1F1F1F1Fu) | (lp[1] + 0x1F1F1F1Fu)) & 0x40404040u; // some L > 32
+	if (__ballot(ov != 0u) == 0ull) {
+#pragma unroll
+		for (uint32_t j = 0; j < 8u; j++)
+			p.put(V[j], len_byte(lp, j));
+		return;
+	}
+#pragma unroll
+	for (uint32_t j = 0; j < 8u; j++) {
+		const uint32_t L = len_byte(lp, j);
+		if (__ballot(L > 32u) == 0ull) {
+			p.put(V[j], L);
+		} else {
+			const bool big = L > 32u;
+			const uint2 ca = rice_code(V[j] & 0xFFFFu, k, tab), cb = rice_code(V[j] >> 16, k, tab);
+			p.put(big ? ca.x : 0u, big ? ca.y : 0u);
+			p.put(big ? cb.x : V[j], big ? cb.y : L);
+		}
+	}
+}
+
+// The look-back (wave 0): the segment's frame bit
+// offset P (header bits included) and the predecessor's last 32 bits.  The
+// first round reads the 16 newest granules and the tail through scalar loads
+// (one asm statement with its wait: no register of an outstanding load is
+// visible to the compiler); further rounds are vector loads of
+// 64 granules, newest first.  Not for the frame's first segment.
+__device__ __forceinline__ uint2 rice_lookback(const KArgs &a, uint32_t gseg, uint32_t sif, uint32_t lane)
+{
+	constexpr uint32_t SLB_N = 16u;
+	const uint32_t first_seg = gseg - sif;
+	uint64_t gv = 0ull, tv = 0ull;
+	bool have = false;
+	if (sif >= SLB_N) {
+		typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+		auto sptr = [](const uint64_t *p) {
+			const uint64_t v = (uint64_t)(uintptr_t)p;
+			const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)v);
+			const uint32_t h = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+			return (const uint64_t *)(uintptr_t)(((uint64_t)h << 32) | l);
+		};
+		const uint64_t *gp = sptr(&a.agg[gseg - SLB_N]);
+		const uint64_t *tp = sptr(&a.tail[gseg - 1u]);
+		u32x16 q0, q1;
+		uint64_t tq;
+		asm volatile("s_load_dwordx16 %0, %3, 0x0 glc\n\t"
+			     "s_load_dwordx16 %1, %3, 0x40 glc\n\t"
+			     "s_load_dwordx2 %2, %4, 0x0 glc\n\t"
+			     "s_waitcnt lgkmcnt(0)"
+			     : "=&s"(q0), "=&s"(q1), "=&s"(tq)
+			     : "s"(gp), "s"(tp)
+			     : "memory");
+		// granule gseg - 16 + i -> lane 15 - i; lanes >= 16 read as unpublished
+		uint32_t vl = 0u, vh = 0u;
+#pragma unroll
+		for (uint32_t i = 0; i < 8u; i++) {
+			vl = lane == 15u - i ? q0[2u * i] : vl;
+			vh = lane == 15u - i ? q0[2u * i + 1u] : vh;
+			vl = lane == 7u - i ? q1[2u * i] : vl;
+			vh = lane == 7u - i ? q1[2u * i + 1u] : vh;
+		}
+		gv = ((uint64_t)vh << 32) | vl;
+		tv = tq;
+		have = true;
+	}
+	if (!have) {
+		const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane;
+		gv = gran_load(&a.agg[idx >= (int64_t)first_seg ? idx : (int64_t)first_seg]);
+		tv = gran_load(&a.tail[gseg - 1u]);
+	}
+	uint32_t sum = 0u, spins = 0u;
+	int64_t j = (int64_t)gseg - 1;
+	for (;;) {
+		const int64_t idx = j - (int64_t)lane;
+		const bool inr = idx >= (int64_t)first_seg;
+		const uint32_t tag = (uint32_t)(gv >> 32);
+		const bool valid = inr && (tag >> 1) == a.epoch;
+		const bool incl = valid && (tag & 1u);
+		const uint64_t incl_m = __ballot(incl);
+		const uint64_t bad_m = __ballot(inr && !valid);
+		const uint32_t fi = incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
+		const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
+		if (!(bad_m & need)) {
+			sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv : 0u);
+			if (incl_m)
+				break;
+			j -= 64; // every granule of this window is an aggregate: the next window
+		} else if (++spins > AIRS_SPIN_LIMIT) {
+			if (lane == 0)
+				atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u); // never expected (the host reports it)
+			break;
+		} else {
+			__builtin_amdgcn_s_sleep(1); // a needed predecessor has not published: re-poll
+		}
+		const int64_t nidx = j - (int64_t)lane;
+		gv = nidx >= (int64_t)first_seg ? gran_load(&a.agg[nidx]) : 0ull;
+	}
+	// the predecessor's tail (lane 0's copy is the one used)
+	for (uint32_t s2 = 0; (uint32_t)(tv >> 32) != a.epoch; s2++) {
+		if (s2 > AIRS_SPIN_LIMIT) {
+			if (lane == 0)
+				atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+			break;
+		}
+		__builtin_amdgcn_s_sleep(1);
+		tv = gran_load(&a.tail[gseg - 1u]);
+	}
+	return make_uint2(sum, (uint32_t)tv);
+}
+
+// Store `tot` bits of an LDS image (bit 0 of word 0 = bit Pc of the frame)
+// to the frame: each complete word funnel-shifted to Pc mod 32, byte-swapped,
+// written through the frame's buffer descriptor (range = capacity rounded
+// down to words, so the hardware drops what does not fit); the final partial
+// word as bytes when `finalx` (reference bitstream_flush).  As
+// encode_kernel's store_chunk.
+__device__ __forceinline__ void rice_store(const uint32_t *Lx, uint32_t Pc, uint32_t totx, uint32_t predx, bool finalx,
+					   __amdgpu_buffer_rsrc_t rsrc, uint8_t *fdst, uint32_t cap, uint32_t tid)
+{
+	if (!totx)
+		return;
+	const uint32_t r = Pc & 31u, g0 = Pc >> 5;
+	const uint32_t endbit = Pc + totx;
+	const uint32_t J = ((endbit - 1u) >> 5) - g0;
+	const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
+	const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)Lx);
+	const uint32_t nquad = nfull >> 2;
+	for (uint32_t p = tid; p < nquad; p += EWG) {
+		const uint32_t j = 4u * p;
+		const u32x4 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + j);
+		const uint32_t hi = j ? Ll[j - 1u] : predx;
+		u32x4 o;
+		o.x = bswap32(__builtin_amdgcn_alignbit(hi, w.x, r));
+		o.y = bswap32(__builtin_amdgcn_alignbit(w.x, w.y, r));
+		o.z = bswap32(__builtin_amdgcn_alignbit(w.y, w.z, r));
+		o.w = bswap32(__builtin_amdgcn_alignbit(w.z, w.w, r));
+		__builtin_amdgcn_raw_buffer_store_b128(o, rsrc, (int)(4u * (g0 + j)), 0, 0);
+	}
+	const uint32_t rr = (tid - nquad) & (EWG - 1u);
+	if (rr < (nfull & 3u)) {
+		const uint32_t j = 4u * nquad + rr;
+		const uint32_t hi = j ? Ll[j - 1u] : predx;
+		__builtin_amdgcn_raw_buffer_store_b32(bswap32(__builtin_amdgcn_alignbit(hi, Ll[j], r)), rsrc,
+						      (int)(4u * (g0 + j)), 0, 0);
+	}
+	if (finalx && nfull == J && tid == 0) {
+		const uint32_t hi = J ? Lx[J - 1u] : predx;
+		const uint32_t v = __builtin_amdgcn_alignbit(hi, Lx[J], r);
+		const uint32_t gw = g0 + J;
+		const uint32_t nbytes = ((endbit & 31u) + 7u) >> 3;
+		for (uint32_t b = 0; b < nbytes; b++)
+			if (4u * gw + b < cap)
+				fdst[4u * gw + b] = (uint8_t)(v >> (24u - 8u * b));
+	}
+}
+
+template <int PRE>
+__global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_WPE, 8))) void rice_kernel(KArgs a)
+{
+	constexpr uint32_t HDR_BITS = 176u; // 22-byte header (GOLOMB_ZERO)
+	extern __shared__ __attribute__((aligned(16))) uint32_t L_ar[]; // RGUARD words, then the arena
+	__shared__ __attribute__((aligned(16))) uint2 s_tab[20];
+	__shared__ __attribute__((aligned(16))) uint32_t s_wsum[2][EWG / 64];
+	__shared__ uint32_t s_misc[4];
+
+	const uint32_t tid = threadIdx.x, lane = tid & 63u;
+	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+	// frame-interleaved dispatch (as encode_kernel): block b is segment b / nfr
+	// of launch frame b % nfr, so a frame's segments are dispatched in order
+	const uint32_t seg = blockIdx.x;
+	const uint32_t nfr = a.num_segs / a.segs_per_frame;
+	const uint32_t sif = seg / nfr, lf = seg - sif * nfr;
+	const uint32_t gseg = lf * a.segs_per_frame + sif;
+	const uint32_t frame =
+		__builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
+	if (frame == AIRS_NO_FRAME)
+		return;
+	const bool is_first = sif == 0u, is_last = sif + 1u == a.segs_per_frame;
+	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
+
+	// ---- phase 0: every load of the segment, then zero the arena ----------
+	uint4 raw[RCH][2];
+	uint32_t prevld[RCH];
+#pragma unroll
+	for (uint32_t c = 0; c < RCH; c++) {
+		const uint32_t first = sif * RSEGN + c * AIRS_SEG + tid * EPT;
+		const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)first * 2u);
+		raw[c][0] = p[0];
+		raw[c][1] = p[1];
+		// the sample before this lane's (lane 0 of each wave uses it): every
+		// lane loads, so the load needs no branch
+		// (0 before the frame's first sample, reference preprocess.c:268-300)
+		if (PRE == PRE_DIFF) {
+			const uint32_t pv = reinterpret_cast<const uint16_t *>(fsrc)[first ? first - 1u : 0u];
+			prevld[c] = first ? pv : 0u;
+		} else {
+			prevld[c] = 0u;
+		}
+	}
+	{
+		uint4 *L4 = reinterpret_cast<uint4 *>(L_ar);
+		for (uint32_t i = tid; i < a.img_words / 4u; i += EWG)
+			L4[i] = make_uint4(0u, 0u, 0u, 0u);
+	}
+	const Coder cd = make_coder<ENC_ZERO>(__builtin_amdgcn_readfirstlane(a.g), a.outlier_param);
+	const uint32_t k = cd.k;
+	if (tid < 18u)
+		s_tab[tid] = rice_table_entry(tid, k);
+	__syncthreads(); // B0: table and zeroed arena
+
+	// ---- phase 1: codeword pairs and lengths -----------------------------
+	// V[c][j]: the codewords of samples 2j, 2j+1 of the lane's chunk c back to
+	// back (or the two mapped values when they exceed 32 bits); lp[c]: the
+	// eight pair lengths, a byte each; T[c]: their sum
+	uint32_t V[RCH][8], lp[RCH][2], T[RCH];
+	const char *tab = reinterpret_cast<const char *>(s_tab);
+#pragma unroll
+	for (uint32_t c = 0; c < RCH; c++) {
+		const uint32_t w[8] = {raw[c][0].x, raw[c][0].y, raw[c][0].z, raw[c][0].w,
+				       raw[c][1].x, raw[c][1].y, raw[c][1].z, raw[c][1].w};
+		uint32_t m[8], q8[8];
+		// the pair ending with the sample before the lane's first: lane i - 1's
+		// last pair (DPP wave_shr:1), lane 0 the loaded sample
+		const uint32_t wprev = PRE == PRE_DIFF ? (uint32_t)__builtin_amdgcn_update_dpp(
+								 (int)(prevld[c] << 16), (int)w[7], 0x138, 0xF, 0xF, false)
+						       : 0u;
+#pragma unroll
+		for (uint32_t j = 0; j < 8u; j++) {
+			uint32_t u = w[j];
+			if (PRE == PRE_DIFF)
+				u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
+			m[j] = zigzag_pk(u);
+			const u16x2 v = __builtin_elementwise_add_sat(pk(m[j]), (u16x2)(1));
+			q8[j] = unpk(__builtin_elementwise_min(v >> (u16x2)((unsigned short)k), (u16x2)(17)) << (u16x2)(3));
+		}
+		uint32_t t = 0u;
+#pragma unroll
+		for (uint32_t h = 0; h < 2u; h++) {
+			uint2 te[8];
+#pragma unroll
+			for (uint32_t jj = 0; jj < 4u; jj++) {
+				const uint32_t j = 4u * h + jj;
+				te[2 * jj] = *reinterpret_cast<const uint2 *>(tab + (q8[j] & 0xFFFFu));
+				te[2 * jj + 1] = *reinterpret_cast<const uint2 *>(tab + (q8[j] >> 16));
+			}
+			uint32_t lw = 0u;
+#pragma unroll
+			for (uint32_t jj = 0; jj < 4u; jj++) {
+				const uint32_t j = 4u * h + jj;
+				const uint2 ea = te[2 * jj], eb = te[2 * jj + 1];
+				const uint32_t cwa = (m[j] & 0xFFFFu) + ea.x, cwb = (m[j] >> 16) + eb.x;
+				const uint32_t L = ea.y + eb.y;
+				// (computed for every pair: a select, not a branch)
+				uint32_t fast = (cwa << eb.y) | cwb;
+				asm volatile("" : "+v"(fast));
+				V[c][j] = L > 32u ? m[j] : fast;
+				t += L;
+				lw = jj ? (lw | (L << (8u * jj))) : L;
+			}
+			lp[c][h] = lw;
+		}
+		T[c] = t;
+		// opaque: keeps the compiler from recomputing the pairs in the packer
+#pragma unroll
+		for (uint32_t j = 0; j < 8u; j++)
+			asm volatile("" : "+v"(V[c][j]));
+	}
+
+	// ---- block scan of the chunk totals (two chunks per register: a wave's
+	// inclusive sums stay below 2^16) --------------------------------------
+	const uint32_t inc01 = wave_incl_scan(T[0] | (T[1] << 16));
+	const uint32_t inc23 = wave_incl_scan(T[2] | (T[3] << 16));
+	if (lane == 63u) {
+		s_wsum[0][wid] = inc01;
+		s_wsum[1][wid] = inc23;
+	}
+
+	// ---- the segment's last 32 bits (wave 3: lanes 60-63, chunk 3) --------
+	if (!is_last && wid == EWG / 64 - 1) {
+		uint64_t acc = 0u;
+		const uint2 *tb = s_tab;
+#pragma unroll
+		for (uint32_t j = 0; j < 8u; j++) {
+			const uint32_t L = len_byte(lp[RCH - 1], j);
+			if (__ballot(L > 32u) == 0ull) {
+				acc = (acc << L) | V[RCH - 1][j];
+			} else {
+				const bool big = L > 32u;
+				const uint2 ca = rice_code(V[RCH - 1][j] & 0xFFFFu, k, tb);
+				const uint2 cb = rice_code(V[RCH - 1][j] >> 16, k, tb);
+				acc = big ? (acc << ca.y) | ca.x : acc;
+				acc = (acc << (big ? cb.y : L)) | (big ? cb.x : V[RCH - 1][j]);
+			}
+		}
+		// (v, t) = the last min(T, 32) bits of a lane run; two scan steps
+		// cover four lanes (>= 32 bits: every sample takes >= k + 1 bits)
+		uint32_t v = (uint32_t)acc, tbits = min(T[RCH - 1], 32u);
+#pragma unroll
+		for (uint32_t d = 1; d <= 2; d <<= 1) {
+			const uint32_t va = __shfl_up(v, d, 64), ta = __shfl_up(tbits, d, 64);
+			if (lane >= d && tbits < 32u) {
+				v = (va << tbits) | v;
+				tbits = min(ta + tbits, 32u);
+			}
+		}
+		if (lane == 63u)
+			gran_store(&a.tail[gseg], ((uint64_t)a.epoch << 32) | v);
+	}
+	__syncthreads(); // B1: wave totals
+
+	uint32_t excl[RCH], tot[RCH], base[RCH];
+	uint32_t A = 0u;
+	{
+		const uint4 s01 = *reinterpret_cast<const uint4 *>(s_wsum[0]);
+		const uint4 s23 = *reinterpret_cast<const uint4 *>(s_wsum[1]);
+		const uint32_t w01[4] = {s01.x, s01.y, s01.z, s01.w}, w23[4] = {s23.x, s23.y, s23.z, s23.w};
+		// chunk totals can pass 2^16 across the four waves: carry-free halves
+		// of each wave's sum, added in 32 bits
+		uint32_t tt[RCH] = {0u, 0u, 0u, 0u}, oo[RCH] = {0u, 0u, 0u, 0u};
+#pragma unroll
+		for (uint32_t w = 0; w < EWG / 64; w++) {
+			tt[0] += w01[w] & 0xFFFFu;
+			tt[1] += w01[w] >> 16;
+			tt[2] += w23[w] & 0xFFFFu;
+			tt[3] += w23[w] >> 16;
+			oo[0] += w < wid ? w01[w] & 0xFFFFu : 0u;
+			oo[1] += w < wid ? w01[w] >> 16 : 0u;
+			oo[2] += w < wid ? w23[w] & 0xFFFFu : 0u;
+			oo[3] += w < wid ? w23[w] >> 16 : 0u;
+		}
+		const uint32_t inc[RCH] = {inc01 & 0xFFFFu, inc01 >> 16, inc23 & 0xFFFFu, inc23 >> 16};
+#pragma unroll
+		for (uint32_t c = 0; c < RCH; c++) {
+			excl[c] = oo[c] + inc[c] - T[c];
+			tot[c] = __builtin_amdgcn_readfirstlane(tt[c]);
+			base[c] = A;
+			A += tot[c];
+		}
+	}
+	if (wid == 0 && lane == 0) {
+		const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
+		gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
+	}
+
+	uint8_t *fdst = a.dst + (uint64_t)frame * a.dst_stride;
+	const uint32_t cap = a.cap;
+	const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(cap & ~3u), 0x00020000);
+	uint32_t *const arena = L_ar + RGUARD;
+	const uint32_t abit = (uint32_t)(uintptr_t)arena << 3; // bit address of the arena in LDS
+	// the segment fits the arena (with a word to spare for a lane's flush)
+	const bool fits = (A >> 5) + 2u <= a.img_words - RGUARD;
+	// header bytes 20-21 (low half of the outlier field) share the frame's
+	// first payload word
+	const uint32_t hdr_pred = cd.outlier & 0xFFFFu;
+	__builtin_amdgcn_s_setprio(1);
+
+	if (fits) {
+		// ---- phase 2: the whole segment into the arena, back to back -----
+#pragma unroll
+		for (uint32_t c = 0; c < RCH; c++) {
+			RPack p;
+			p.init(abit + base[c] + excl[c]);
+			pack_chunk(p, V[c], lp[c], k, s_tab);
+			p.flush();
+		}
+		if (wid == 0) {
+			uint2 pp = make_uint2(HDR_BITS, hdr_pred);
+			if (!is_first)
+				pp = rice_lookback(a, gseg, sif, lane);
+			if (lane == 0) {
+				if (!is_first)
+					gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (pp.x + A));
+				s_misc[0] = pp.x;
+				s_misc[1] = pp.y;
+			}
+		}
+		__syncthreads(); // B2: arena complete, offset known
+		const uint32_t P = __builtin_amdgcn_readfirstlane(s_misc[0]);
+		const uint32_t pred = __builtin_amdgcn_readfirstlane(s_misc[1]);
+		rice_store(arena, P, A, pred, is_last, rsrc, fdst, cap, tid);
+		if (is_last && tid == 0)
+			s_misc[2] = P;
+	} else {
+		// ---- a segment that does not fit: offset first, then chunk by chunk
+		// through the arena (every chunk fits: 4096 x (k + 17) bits) --------
+		if (wid == 0) {
+			uint2 pp = make_uint2(HDR_BITS, hdr_pred);
+			if (!is_first)
+				pp = rice_lookback(a, gseg, sif, lane);
+			if (lane == 0) {
+				if (!is_first)
+					gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (pp.x + A));
+				s_misc[0] = pp.x;
+				s_misc[1] = pp.y;
+			}
+		}
+		__syncthreads();
+		const uint32_t P = __builtin_amdgcn_readfirstlane(s_misc[0]);
+		uint32_t pred = __builtin_amdgcn_readfirstlane(s_misc[1]);
+		uint32_t last_ne = 0u;
+#pragma unroll
+		for (uint32_t c = 0; c < RCH; c++)
+			last_ne = tot[c] ? c : last_ne;
+#pragma unroll
+		for (uint32_t c = 0; c < RCH; c++) {
+			RPack p;
+			p.init(abit + excl[c]);
+			pack_chunk(p, V[c], lp[c], k, s_tab);
+			p.flush();
+			__syncthreads();
+			rice_store(arena, P + base[c], tot[c], pred, is_last && c == last_ne, rsrc, fdst, cap, tid);
+			// the last 32 bits of this chunk precede the next one
+			if (tot[c] >= 32u) {
+				const uint32_t s0 = tot[c] - 32u, q = s0 >> 5, sh = s0 & 31u;
+				pred = sh ? (arena[q] << sh) | (arena[q + 1] >> (32u - sh)) : arena[q];
+			} else if (tot[c]) {
+				pred = (pred << tot[c]) | (arena[0] >> (32u - tot[c]));
+			}
+			__syncthreads();
+			for (uint32_t i = tid; i < ((tot[c] + 31u) >> 5) + 1u; i += EWG)
+				arena[i] = 0u;
+			__syncthreads();
+		}
+		if (is_last && tid == 0)
+			s_misc[2] = P;
+	}
+
+	// ---- frame epilogue: checksum, header, status (the frame's last
+	// segment; as encode_kernel) ------------------------------------------
+	if (is_last && tid == 0) {
+		const uint32_t P = s_misc[2];
+		const uint32_t n = a.n;
+		const uint32_t payload_bytes = (P + A + 7u) >> 3;
+		const uint32_t size = payload_bytes + (a.checksum ? 4u : 0u);
+		if (a.checksum) {
+			const uint32_t ck = a.checksums[frame];
+			for (uint32_t b = 0; b < 4u; b++)
+				if (payload_bytes + b < cap)
+					fdst[payload_bytes + b] = (uint8_t)(ck >> (24u - 8u * b));
+		}
+		const uint64_t id = a.ids ? a.ids[lf] : a.id_base + (uint64_t)lf * a.id_step;
+		uint32_t h[5];
+		header_words(h, size, 2u * n, id, a.seqs ? a.seqs[frame] : a.seq, PRE, a.checksum ? 1u : 0u, ENC_ZERO, 0u,
+			     cd.g, cd.outlier);
+		if (((uintptr_t)fdst & 7u) == 0u && cap >= 20u) {
+			*reinterpret_cast<uint2 *>(fdst) = make_uint2(bswap32(h[0]), bswap32(h[1]));
+			*reinterpret_cast<uint2 *>(fdst + 8) = make_uint2(bswap32(h[2]), bswap32(h[3]));
+			*reinterpret_cast<uint32_t *>(fdst + 16) = bswap32(h[4]);
+		} else {
+#pragma unroll
+			for (uint32_t w = 0; w < 5u; w++)
+				if (4u * w + 4u <= cap)
+					*reinterpret_cast<uint32_t *>(fdst + 4u * w) = bswap32(h[w]);
+		}
+		uint32_t st = size;
+		if (size > cap)
+			st = ERRV(E_DST_TOO_SMALL);
+		else if (size > 0xFFFFFFu)
+			st = ERRV(E_HDR_CMP_SIZE_TOO_LARGE);
+		a.status[frame] = st;
+		if (a.needed)
+			a.needed[frame] = size;
+	}
+}
+
+// The launch, or false when it does not fit this kernel (the caller then
+// takes encode_kernel): 16-bit NONE/DIFF GOLOMB_ZERO with one g = 2^k,
+// k <= RICE_KMAX, for every frame, no model, whole segments of 16 Ki samples.
+bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s)
+{
+	if (pre != PRE_NONE && pre != PRE_DIFF)
+		return false;
+	if (k.frame_g || k.ktot || k.model_mode || !k.g || (k.g & (k.g - 1u)) || k.g > (1u << RICE_KMAX))
+		return false;
+	if (k.segs_per_frame == 0u || k.n != k.segs_per_frame * RSEGN)
+		return false;
+	KArgs ka = k;
+	ka.img_words = rice_arena_words();
+	const size_t lds = (size_t)ka.img_words * 4u;
+	if (pre == PRE_DIFF)
+		hipLaunchKernelGGL(rice_kernel<PRE_DIFF>, dim3(k.num_segs), dim3(EWG), lds, s, ka);
+	else
+		hipLaunchKernelGGL(rice_kernel<PRE_NONE>, dim3(k.num_segs), dim3(EWG), lds, s, ka);
+	return true;
+}
+
+} // namespace airs

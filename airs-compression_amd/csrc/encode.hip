@@ -1188,6 +1188,15 @@ static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t 
 			return;
 		}
 	}
+#ifndef AIRS_RICE
+#define AIRS_RICE 1
+#endif
+	// the Rice/ZERO frame kernel (enc_rice.hip)
+	if constexpr (AIRS_RICE && W == 2 && (PRE == PRE_NONE || PRE == PRE_DIFF) && ENC == ENC_ZERO && RICE &&
+		      MODEL == 0) {
+		if (full && rice_encode(k, PRE, s))
+			return;
+	}
 	// the arena kernel (enc_arena.hip): 16-bit NONE/DIFF, Rice ZERO with
 	// k <= 11 for every frame, no model, whole aligned segments
 	if constexpr (W == 2 && (PRE == PRE_NONE || PRE == PRE_DIFF) && ENC == ENC_ZERO && RICE && MODEL == 0) {

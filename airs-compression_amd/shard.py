@@ -173,6 +173,24 @@ def check_patchable(params, draws, layout: str = "roundrobin") -> None:
                          f"secondary pass, which depends on its rank's previous frame); use the 'streams' layout")
 
 
+def check_patchable_all(dist, params, draws, layout: str, device, group=None) -> None:
+    """check_patchable on every rank, decided together: each rank
+    checks its own draws and parameters, and one all_reduce(MAX) of the
+    refusal flag makes every rank raise if any rank refuses, so no rank is
+    left waiting in a barrier or the gather while a peer has raised."""
+    err = None
+    try:
+        check_patchable(params, draws, layout)
+    except ValueError as e:
+        err = e
+    flag = torch.tensor([1 if err is not None else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if int(flag.item()):
+        raise err if err is not None else ValueError(
+            f"identifier patching of the {layout!r} layout refused on another rank (its draw counts show a "
+            f"secondary pass, or its parameters do); use the 'streams' layout")
+
+
 def assign_identifiers(draws: torch.Tensor, base: int, layout: str, fpc: int = 1) -> tuple[torch.Tensor, torch.Tensor]:
     """Identifiers of frames in global order from their draw counts (int64,
     global order): (ids, keep) with ids[g] = base + inclusive scan of the
@@ -316,7 +334,8 @@ def gather_frames_timed(dist, dst, dst_stride, sizes, num_frames, rank, world, r
     (stats dict, GatheredFrames or None)."""
     cuda = dst.is_cuda
     if patch_base is not None:
-        check_patchable(params, draws, layout)  # on every rank, before any communication
+        # on every rank, before any other communication, decided together
+        check_patchable_all(dist, params, draws, layout, dst.device)
 
     def sync():
         if cuda:

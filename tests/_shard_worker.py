@@ -194,6 +194,20 @@ def run(rank, world, port, nf, n, layout, mode):
                 else:
                     raise AssertionError("patching a frame layout with secondary passes was not refused")
             return
+        if mode == "patch_refused_one_rank":
+            # only rank 1's draws show a secondary pass (a 0): every rank must
+            # raise, none may wait in the gather
+            d = torch.ones(nf, dtype=torch.uint8)
+            if rank == 1:
+                d[nf // 2] = 0
+            try:
+                shard.gather_frames_timed(dist, dst_t, stride, sizes_t, nf, rank, world, layout=layout,
+                                          patch_base=0, params=None, draws=d)
+            except ValueError as e:
+                assert ("secondary" in str(e)) or ("another rank" in str(e)), str(e)
+            else:
+                raise AssertionError(f"rank {rank}: a refusal on rank 1 alone did not stop this rank")
+            return
         if mode == "patch_refused":
             try:
                 shard.gather_frames_timed(dist, dst_t, stride, sizes_t, nf, rank, world, layout=layout,

@@ -50,6 +50,13 @@ def test_gather_world2_patch_refused_with_draws_and_secondary_passes(orc, layout
     _spawn(3, 500, layout, "patch_refused_draws")
 
 
+@pytest.mark.parametrize("layout", ["roundrobin", "block"])
+def test_gather_world2_patch_refused_on_one_rank_only(orc, layout):
+    """Only one rank's draw counts hold a 0 (a secondary pass): the refusal is
+    collective, every rank raises before the gather."""
+    _spawn(3, 500, layout, "patch_refused_one_rank")
+
+
 def test_gather_world2_fallback_identifiers_vs_one_context(orc):
     """Round-robin frames with the uncompressed fallback (three draws per
     fallback frame): after the gather every frame, identifier included, equals
