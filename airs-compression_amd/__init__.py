@@ -22,6 +22,9 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libairscmp.so")
 GPU_U16, GPU_I16, GPU_I16_IN_I32 = 0, 1, 2
 GPU_AUTO_RICE = 0x1
 REPORT_DRAWS = 0x8  # CMP_GPU_REPORT_DRAWS
+OPT_EXCLUSIVE = 1  # cmp_gpu_engine_set_option (include/cmp_gpu.h)
+OPT_WALK_SEGMENT = 2
+OPT_NO_CONTEXT_WALK = 3
 KIND_TO_GPU = {"u16": GPU_U16, "i16": GPU_I16, "i16_in_i32": GPU_I16_IN_I32}
 
 
@@ -97,6 +100,8 @@ class AirsLib(CmpLib):
         L.cmp_gpu_engine_create.restype = c_uint32
         L.cmp_gpu_engine_destroy.argtypes = [c_void_p]
         L.cmp_gpu_engine_destroy.restype = None
+        L.cmp_gpu_engine_set_option.argtypes = [c_void_p, c_uint32, c_uint32]
+        L.cmp_gpu_engine_set_option.restype = c_uint32
         L.cmp_gpu_compress.argtypes = [c_void_p, POINTER(CmpContext), c_uint32, c_uint32, POINTER(GpuBatch)]
         L.cmp_gpu_compress.restype = c_uint32
         L.cmp_gpu_synchronize.argtypes = [c_void_p]
@@ -131,6 +136,10 @@ class GpuEngine:
         if is_error(r):
             raise RuntimeError(f"cmp_gpu_engine_create failed: {error_name(r)}")
         self.handle = h
+
+    def set_option(self, option: int, value: int) -> int:
+        """cmp_gpu_engine_set_option (OPT_EXCLUSIVE, OPT_WALK_SEGMENT, OPT_NO_CONTEXT_WALK)."""
+        return int(self.lib.lib.cmp_gpu_engine_set_option(self.handle, option, value))
 
     def close(self):
         if self.handle:

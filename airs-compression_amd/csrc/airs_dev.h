@@ -86,6 +86,11 @@ struct airs_dev_engine;
 
 /* create an engine on the current HIP device; stream = hipStream_t or NULL (default) */
 struct airs_dev_engine *airs_dev_engine_create(void *stream);
+/* engine options (cmp_gpu_engine_set_option): 0 or an error value */
+#define AIRS_OPT_EXCLUSIVE 1u
+#define AIRS_OPT_WALK_SEGMENT 2u
+#define AIRS_OPT_NO_CONTEXT_WALK 3u
+uint32_t airs_dev_set_option(struct airs_dev_engine *e, uint32_t option, uint32_t value);
 void airs_dev_engine_destroy(struct airs_dev_engine *e);
 void *airs_dev_engine_stream(struct airs_dev_engine *e);
 

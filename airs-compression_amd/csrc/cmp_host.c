@@ -617,6 +617,13 @@ uint32_t cmp_gpu_engine_create(struct cmp_gpu_engine **engine, void *hip_stream)
 	return 0;
 }
 
+uint32_t cmp_gpu_engine_set_option(struct cmp_gpu_engine *engine, uint32_t option, uint32_t value)
+{
+	if (!engine)
+		return ERRV(GENERIC);
+	return airs_dev_set_option(engine->dev, option, value);
+}
+
 void cmp_gpu_engine_destroy(struct cmp_gpu_engine *engine)
 {
 	if (!engine)

@@ -496,30 +496,18 @@ struct WArgs {
 // the segment walk: < 0 no kernel for these passes; 0 launched with the
 // ticket (the caller advances its ticket base); 1 launched direct
 int walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
-		 bool rice_s, hipStream_t s);
+		 bool rice_s, hipStream_t s, bool exclusive);
 // one context per workgroup (frames of walk_ctx_samples() samples); img_words
 // = words of ONE of its two 16384-sample images
 bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p,
 		     uint32_t enc_s, bool rice_s, hipStream_t s);
 uint32_t walk_ctx_samples();
-// the frame walk with the per-frame Rice k (64 Ki-sample 16-bit frames, NONE/DIFF):
-// false when the launch does not fit it
-bool frame_auto_encode(const KArgs &k, uint32_t pre, hipStream_t s);
 // samples per segment of the segment walk (walk_kernel): 4096 with four data
 // waves, 2048 with two (batches of few contexts); k.spf = n / that
 uint32_t walk_seg_samples(bool half);
-// the arena kernel (enc_arena.hip): 16-bit NONE/DIFF GOLOMB_ZERO g = 2^k <=
-// 2048, no model, whole segments; k.img_words = arena_words()
-bool arena_encode(const KArgs &k, uint32_t pre, bool stream, uint32_t grid, hipStream_t s);
 // the Rice/ZERO frame kernel (enc_rice.hip): 16-bit NONE/DIFF, one g = 2^k
 // (k <= 7), no model, whole 16 Ki-sample segments; false: not eligible
 bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s);
-uint32_t arena_words();
-bool arena_enabled();
-// AUTO (fused per-frame Rice k) launches of frames of whole 16 Ki-sample
-// segments, 16-bit NONE/DIFF: grid padded to whole groups of 8 frames
-bool arena_auto_encode(const KArgs &k, uint32_t pre, uint32_t grid, hipStream_t s);
-bool arena_auto_enabled();
 void stream_encode(const KArgs &k, uint32_t sample_bytes, uint32_t pre, uint32_t enc, bool rice, bool full,
 		   uint32_t grid, hipStream_t s);
 

@@ -38,20 +38,34 @@
 
 namespace airs {
 
-#ifndef AIRS_RICE_WPE // workgroups (= waves per SIMD) per CU the kernel is built for
-#define AIRS_RICE_WPE 5
+#ifndef AIRS_RICE_WG // threads per workgroup (256 or 512)
+#define AIRS_RICE_WG 256
+#endif
+#ifndef AIRS_RICE_WGPCU // workgroups per CU the LDS (and register allocation) is sized for
+#define AIRS_RICE_WGPCU 4
+#endif
+#define AIRS_RICE_WPE (AIRS_RICE_WGPCU * AIRS_RICE_WG / 256) // waves per SIMD
+#ifndef AIRS_RICE_LBC // the look-back is evaluated after packing this many chunks (wave 0)
+#define AIRS_RICE_LBC 4
+#endif
+#ifndef AIRS_RICE_SLB // granules of the scalar first look-back round (16 or 32)
+#define AIRS_RICE_SLB 16
 #endif
 #define RICE_KMAX 7u       // largest k this kernel takes (pairs of typical codes fit 32 bits)
-constexpr uint32_t RCH = 4u;                 // chunks of AIRS_SEG samples per segment
-constexpr uint32_t RSEGN = RCH * AIRS_SEG;   // 16384 samples per segment
+constexpr uint32_t RWG = AIRS_RICE_WG;      // threads per workgroup
+constexpr uint32_t RNW = RWG / 64u;         // waves per workgroup
+constexpr uint32_t RCHUNK = RWG * 16u;      // samples per chunk: lane t owns [16t, 16t+16)
+constexpr uint32_t RCH = 4u;                // chunks per segment
+constexpr uint32_t RSEGN = RCH * RCHUNK;    // samples per segment (16 Ki or 32 Ki)
 constexpr uint32_t RGUARD = 4u;              // words before the arena (a lane's first put ORs zeros there)
-constexpr uint32_t RSTATIC = 512u;           // static LDS of the kernel, rounded up
-static_assert(EPT == 16u, "lane t owns samples [16t, 16t+16) of each chunk");
+// LDS per workgroup is allocated in granules: leave room for the static LDS
+// and the rounding (measured: a 32464-byte workgroup admitted only four per CU)
+constexpr uint32_t RSTATIC = 2048u;
 
 // arena words (guard included) for AIRS_RICE_WPE workgroups per CU
 __host__ __device__ constexpr uint32_t rice_arena_words()
 {
-	return ((160u * 1024u / AIRS_RICE_WPE - RSTATIC) / 4u) & ~3u;
+	return ((160u * 1024u / AIRS_RICE_WGPCU - RSTATIC) / 4u) & ~3u;
 }
 
 // the four words of a lane's chunk: lengths of pairs 4h .. 4h+3, a byte each
@@ -130,9 +144,11 @@ __device__ __forceinline__ void pack_chunk(RPack &p, const uint32_t (&V)[8], con
 // (one asm statement with its wait: no register of an outstanding load is
 // visible to the compiler); further rounds are vector loads of
 // 64 granules, newest first.  Not for the frame's first segment.
-__device__ __forceinline__ uint2 rice_lookback(const KArgs &a, uint32_t gseg, uint32_t sif, uint32_t lane)
+__device__ __forceinline__ uint2 rice_lookback(const KArgs &a, uint32_t gseg, uint32_t sif, uint32_t lane,
+					       uint64_t gearly)
 {
-	constexpr uint32_t SLB_N = 16u;
+	uint32_t rounds = 1u;
+	constexpr uint32_t SLB_N = AIRS_RICE_SLB;
 	const uint32_t first_seg = gseg - sif;
 	uint64_t gv = 0ull, tv = 0ull;
 	bool have = false;
@@ -146,23 +162,35 @@ __device__ __forceinline__ uint2 rice_lookback(const KArgs &a, uint32_t gseg, ui
 		};
 		const uint64_t *gp = sptr(&a.agg[gseg - SLB_N]);
 		const uint64_t *tp = sptr(&a.tail[gseg - 1u]);
-		u32x16 q0, q1;
+		// q[b]: granules gseg - SLB_N + 8 b .. + 7 -> lanes SLB_N - 1 - (8 b + i);
+		// lanes >= SLB_N read as unpublished
+		u32x16 q[SLB_N / 8u];
 		uint64_t tq;
-		asm volatile("s_load_dwordx16 %0, %3, 0x0 glc\n\t"
-			     "s_load_dwordx16 %1, %3, 0x40 glc\n\t"
-			     "s_load_dwordx2 %2, %4, 0x0 glc\n\t"
-			     "s_waitcnt lgkmcnt(0)"
-			     : "=&s"(q0), "=&s"(q1), "=&s"(tq)
-			     : "s"(gp), "s"(tp)
-			     : "memory");
-		// granule gseg - 16 + i -> lane 15 - i; lanes >= 16 read as unpublished
-		uint32_t vl = 0u, vh = 0u;
+		if constexpr (SLB_N == 32u)
+			asm volatile("s_load_dwordx16 %0, %5, 0x0 glc\n\t"
+				     "s_load_dwordx16 %1, %5, 0x40 glc\n\t"
+				     "s_load_dwordx16 %2, %5, 0x80 glc\n\t"
+				     "s_load_dwordx16 %3, %5, 0xc0 glc\n\t"
+				     "s_load_dwordx2 %4, %6, 0x0 glc\n\t"
+				     "s_waitcnt lgkmcnt(0)"
+				     : "=&s"(q[0]), "=&s"(q[1]), "=&s"(q[2]), "=&s"(q[3]), "=&s"(tq)
+				     : "s"(gp), "s"(tp)
+				     : "memory");
+		else
+			asm volatile("s_load_dwordx16 %0, %3, 0x0 glc\n\t"
+				     "s_load_dwordx16 %1, %3, 0x40 glc\n\t"
+				     "s_load_dwordx2 %2, %4, 0x0 glc\n\t"
+				     "s_waitcnt lgkmcnt(0)"
+				     : "=&s"(q[0]), "=&s"(q[1]), "=&s"(tq)
+				     : "s"(gp), "s"(tp)
+				     : "memory");
+		// lanes >= SLB_N: the window read when the aggregate was published
+		// (granules gseg - 1 - lane; any published value stays true)
+		uint32_t vl = (uint32_t)gearly, vh = (uint32_t)(gearly >> 32);
 #pragma unroll
-		for (uint32_t i = 0; i < 8u; i++) {
-			vl = lane == 15u - i ? q0[2u * i] : vl;
-			vh = lane == 15u - i ? q0[2u * i + 1u] : vh;
-			vl = lane == 7u - i ? q1[2u * i] : vl;
-			vh = lane == 7u - i ? q1[2u * i + 1u] : vh;
+		for (uint32_t i = 0; i < SLB_N; i++) {
+			vl = lane == SLB_N - 1u - i ? q[i >> 3][2u * (i & 7u)] : vl;
+			vh = lane == SLB_N - 1u - i ? q[i >> 3][2u * (i & 7u) + 1u] : vh;
 		}
 		gv = ((uint64_t)vh << 32) | vl;
 		tv = tq;
@@ -190,18 +218,21 @@ __device__ __forceinline__ uint2 rice_lookback(const KArgs &a, uint32_t gseg, ui
 			if (incl_m)
 				break;
 			j -= 64; // every granule of this window is an aggregate: the next window
+			rounds++;
 		} else if (++spins > AIRS_SPIN_LIMIT) {
 			if (lane == 0)
 				atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u); // never expected (the host reports it)
 			break;
 		} else {
 			__builtin_amdgcn_s_sleep(1); // a needed predecessor has not published: re-poll
+			rounds++;
 		}
 		const int64_t nidx = j - (int64_t)lane;
 		gv = nidx >= (int64_t)first_seg ? gran_load(&a.agg[nidx]) : 0ull;
 	}
 	// the predecessor's tail (lane 0's copy is the one used)
-	for (uint32_t s2 = 0; (uint32_t)(tv >> 32) != a.epoch; s2++) {
+	uint32_t s2 = 0;
+	for (; (uint32_t)(tv >> 32) != a.epoch; s2++) {
 		if (s2 > AIRS_SPIN_LIMIT) {
 			if (lane == 0)
 				atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
@@ -209,6 +240,10 @@ __device__ __forceinline__ uint2 rice_lookback(const KArgs &a, uint32_t gseg, ui
 		}
 		__builtin_amdgcn_s_sleep(1);
 		tv = gran_load(&a.tail[gseg - 1u]);
+	}
+	if (DBG(65536u) && a.dbgts && lane == 0) {
+		a.dbgts[8u * gseg + 5u] = ((uint64_t)spins << 32) | rounds;
+		a.dbgts[8u * gseg + 6u] = s2;
 	}
 	return make_uint2(sum, (uint32_t)tv);
 }
@@ -230,7 +265,7 @@ __device__ __forceinline__ void rice_store(const uint32_t *Lx, uint32_t Pc, uint
 	const uint32_t nfull = (endbit & 31u) == 0u ? J + 1u : J;
 	const lds_u32 *Ll = reinterpret_cast<const lds_u32 *>((uintptr_t)Lx);
 	const uint32_t nquad = nfull >> 2;
-	for (uint32_t p = tid; p < nquad; p += EWG) {
+	for (uint32_t p = tid; p < nquad; p += RWG) {
 		const uint32_t j = 4u * p;
 		const u32x4 w = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(Ll + j);
 		const uint32_t hi = j ? Ll[j - 1u] : predx;
@@ -241,7 +276,7 @@ __device__ __forceinline__ void rice_store(const uint32_t *Lx, uint32_t Pc, uint
 		o.w = bswap32(__builtin_amdgcn_alignbit(w.z, w.w, r));
 		__builtin_amdgcn_raw_buffer_store_b128(o, rsrc, (int)(4u * (g0 + j)), 0, 0);
 	}
-	const uint32_t rr = (tid - nquad) & (EWG - 1u);
+	const uint32_t rr = (tid - nquad) & (RWG - 1u);
 	if (rr < (nfull & 3u)) {
 		const uint32_t j = 4u * nquad + rr;
 		const uint32_t hi = j ? Ll[j - 1u] : predx;
@@ -259,42 +294,32 @@ __device__ __forceinline__ void rice_store(const uint32_t *Lx, uint32_t Pc, uint
 	}
 }
 
+// the lane's samples of segment `sif` of a frame: 4 chunks x 16 samples, and
+// for DIFF the sample before each chunk's first (lane 0 of each wave uses it;
+// every lane loads, so the load needs no branch; 0 before the frame's first
+// sample, reference preprocess.c:268-300)
 template <int PRE>
-__global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_WPE, 8))) void rice_kernel(KArgs a)
+__device__ __forceinline__ void rice_load(const KArgs &a, const uint8_t *fsrc, uint32_t sif, uint32_t gseg, uint32_t tid,
+					  uint4 (&raw)[RCH][2], uint32_t (&prevld)[RCH])
 {
-	constexpr uint32_t HDR_BITS = 176u; // 22-byte header (GOLOMB_ZERO)
-	extern __shared__ __attribute__((aligned(16))) uint32_t L_ar[]; // RGUARD words, then the arena
-	__shared__ __attribute__((aligned(16))) uint2 s_tab[20];
-	__shared__ __attribute__((aligned(16))) uint32_t s_wsum[2][EWG / 64];
-	__shared__ uint32_t s_misc[4];
-
-	const uint32_t tid = threadIdx.x, lane = tid & 63u;
-	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-	// frame-interleaved dispatch (as encode_kernel): block b is segment b / nfr
-	// of launch frame b % nfr, so a frame's segments are dispatched in order
-	const uint32_t seg = blockIdx.x;
-	const uint32_t nfr = a.num_segs / a.segs_per_frame;
-	const uint32_t sif = seg / nfr, lf = seg - sif * nfr;
-	const uint32_t gseg = lf * a.segs_per_frame + sif;
-	const uint32_t frame =
-		__builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
-	if (frame == AIRS_NO_FRAME)
-		return;
-	const bool is_first = sif == 0u, is_last = sif + 1u == a.segs_per_frame;
-	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
-
-	// ---- phase 0: every load of the segment, then zero the arena ----------
-	uint4 raw[RCH][2];
-	uint32_t prevld[RCH];
 #pragma unroll
 	for (uint32_t c = 0; c < RCH; c++) {
-		const uint32_t first = sif * RSEGN + c * AIRS_SEG + tid * EPT;
+		const uint32_t first = sif * RSEGN + c * RCHUNK + tid * EPT;
 		const uint4 *p = reinterpret_cast<const uint4 *>(fsrc + (size_t)first * 2u);
-		raw[c][0] = p[0];
-		raw[c][1] = p[1];
-		// the sample before this lane's (lane 0 of each wave uses it): every
-		// lane loads, so the load needs no branch
-		// (0 before the frame's first sample, reference preprocess.c:268-300)
+		if (DBG(512u)) { // ablation: no HBM reads (noise of width ~64 made in registers)
+			uint32_t h = (first * 2654435761u) ^ (gseg * 40503u);
+			uint32_t wv[8];
+#pragma unroll
+			for (uint32_t q = 0; q < 8u; q++) {
+				h = h * 1664525u + 1013904223u;
+				wv[q] = 0x40004000u + ((h >> 8) & 0x003F003Fu);
+			}
+			raw[c][0] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+			raw[c][1] = make_uint4(wv[4], wv[5], wv[6], wv[7]);
+		} else {
+			raw[c][0] = p[0];
+			raw[c][1] = p[1];
+		}
 		if (PRE == PRE_DIFF) {
 			const uint32_t pv = reinterpret_cast<const uint16_t *>(fsrc)[first ? first - 1u : 0u];
 			prevld[c] = first ? pv : 0u;
@@ -302,9 +327,42 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 			prevld[c] = 0u;
 		}
 	}
+}
+
+template <int PRE, bool PERSIST>
+__global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_WPE, 8))) void rice_kernel(KArgs a)
+{
+	constexpr uint32_t HDR_BITS = 176u; // 22-byte header (GOLOMB_ZERO)
+	extern __shared__ __attribute__((aligned(16))) uint32_t L_ar[]; // RGUARD words, then the arena
+	__shared__ __attribute__((aligned(16))) uint2 s_tab[20];
+	__shared__ __attribute__((aligned(16))) uint32_t s_wsum[2][RNW];
+	__shared__ uint32_t s_misc[4];
+
+	const uint32_t tid = threadIdx.x, lane = tid & 63u;
+	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const uint32_t nfr = a.num_segs / a.segs_per_frame;
+	// Frame-interleaved order (as encode_kernel): dispatch index d is segment
+	// d / nfr of launch frame d % nfr, so a frame's segments come in order.
+	// One segment per workgroup, d = the block index; PERSIST (experiment):
+	// workgroup b walks d = b, b + G, b + 2G, ... (G = the grid, all of it
+	// resident) with the next segment's samples loaded during this one's
+	// packing, look-back and stores.
+	uint32_t d = blockIdx.x;
+	uint32_t sif = d / nfr, lf = d - sif * nfr;
+	uint32_t gseg = lf * a.segs_per_frame + sif;
+	uint32_t frame = __builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
+	if (frame == AIRS_NO_FRAME)
+		return;
+	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
+	dbg_stamp(a, gseg, 0);
+
+	// ---- phase 0: every load of the segment, then zero the arena ----------
+	uint4 raw[RCH][2];
+	uint32_t prevld[RCH];
+	rice_load<PRE>(a, fsrc, sif, gseg, tid, raw, prevld);
 	{
 		uint4 *L4 = reinterpret_cast<uint4 *>(L_ar);
-		for (uint32_t i = tid; i < a.img_words / 4u; i += EWG)
+		for (uint32_t i = tid; i < a.img_words / 4u; i += RWG)
 			L4[i] = make_uint4(0u, 0u, 0u, 0u);
 	}
 	const Coder cd = make_coder<ENC_ZERO>(__builtin_amdgcn_readfirstlane(a.g), a.outlier_param);
@@ -313,6 +371,8 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		s_tab[tid] = rice_table_entry(tid, k);
 	__syncthreads(); // B0: table and zeroed arena
 
+	for (;;) {
+	const bool is_first = sif == 0u, is_last = sif + 1u == a.segs_per_frame;
 	// ---- phase 1: codeword pairs and lengths -----------------------------
 	// V[c][j]: the codewords of samples 2j, 2j+1 of the lane's chunk c back to
 	// back (or the two mapped values when they exceed 32 bits); lp[c]: the
@@ -371,6 +431,19 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 			asm volatile("" : "+v"(V[c][j]));
 	}
 
+	// PERSIST: the next segment's samples, in flight from here on
+	const uint32_t dn = d + gridDim.x;
+	uint32_t sif_n = 0u, lf_n = 0u, frame_n = 0u;
+	const uint8_t *fsrc_n = fsrc;
+	if (PERSIST) {
+		const uint32_t dl = dn < a.num_segs ? dn : d; // (past the end: this segment again, unused)
+		sif_n = dl / nfr;
+		lf_n = dl - sif_n * nfr;
+		frame_n = __builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf_n] : a.frame_add + lf_n * a.frame_mul);
+		fsrc_n = a.src + (uint64_t)frame_n * a.src_stride;
+		rice_load<PRE>(a, fsrc_n, sif_n, gseg, tid, raw, prevld);
+	}
+
 	// ---- block scan of the chunk totals (two chunks per register: a wave's
 	// inclusive sums stay below 2^16) --------------------------------------
 	const uint32_t inc01 = wave_incl_scan(T[0] | (T[1] << 16));
@@ -381,7 +454,7 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 	}
 
 	// ---- the segment's last 32 bits (wave 3: lanes 60-63, chunk 3) --------
-	if (!is_last && wid == EWG / 64 - 1) {
+	if (!is_last && wid == RNW - 1) {
 		uint64_t acc = 0u;
 		const uint2 *tb = s_tab;
 #pragma unroll
@@ -411,19 +484,29 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		if (lane == 63u)
 			gran_store(&a.tail[gseg], ((uint64_t)a.epoch << 32) | v);
 	}
+	if (DBG(32768u)) { // ablation: stop after phase 1
+		if (T[0] == 0x12345u && tid == 999u)
+			a.status[0] = V[0][0] + V[RCH - 1][1] + lp[1][1];
+		return;
+	}
 	__syncthreads(); // B1: wave totals
 
 	uint32_t excl[RCH], tot[RCH], base[RCH];
 	uint32_t A = 0u;
 	{
-		const uint4 s01 = *reinterpret_cast<const uint4 *>(s_wsum[0]);
-		const uint4 s23 = *reinterpret_cast<const uint4 *>(s_wsum[1]);
-		const uint32_t w01[4] = {s01.x, s01.y, s01.z, s01.w}, w23[4] = {s23.x, s23.y, s23.z, s23.w};
+		uint32_t w01[RNW], w23[RNW];
+#pragma unroll
+		for (uint32_t w = 0; w < RNW; w += 4) {
+			const uint4 s01 = *reinterpret_cast<const uint4 *>(&s_wsum[0][w]);
+			const uint4 s23 = *reinterpret_cast<const uint4 *>(&s_wsum[1][w]);
+			w01[w] = s01.x, w01[w + 1] = s01.y, w01[w + 2] = s01.z, w01[w + 3] = s01.w;
+			w23[w] = s23.x, w23[w + 1] = s23.y, w23[w + 2] = s23.z, w23[w + 3] = s23.w;
+		}
 		// chunk totals can pass 2^16 across the four waves: carry-free halves
 		// of each wave's sum, added in 32 bits
 		uint32_t tt[RCH] = {0u, 0u, 0u, 0u}, oo[RCH] = {0u, 0u, 0u, 0u};
 #pragma unroll
-		for (uint32_t w = 0; w < EWG / 64; w++) {
+		for (uint32_t w = 0; w < RNW; w++) {
 			tt[0] += w01[w] & 0xFFFFu;
 			tt[1] += w01[w] >> 16;
 			tt[2] += w23[w] & 0xFFFFu;
@@ -446,6 +529,19 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
 		gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
 	}
+	dbg_stamp(a, gseg, 1);
+	// The look-back's window of 64 granules, read now and evaluated after the
+	// packing (wave 0, frames of >= 16 predecessors): the older granules of
+	// the window are mostly published by now, the 16 newest are read again
+	// by the scalar round at evaluation
+	uint64_t gearly = 0ull;
+#ifndef AIRS_RICE_EARLY
+#define AIRS_RICE_EARLY 0
+#endif
+	if (AIRS_RICE_EARLY && wid == 0 && sif >= AIRS_RICE_SLB) {
+		const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane, fs = (int64_t)(gseg - sif);
+		gearly = gran_load(&a.agg[idx >= fs ? idx : fs]);
+	}
 
 	uint8_t *fdst = a.dst + (uint64_t)frame * a.dst_stride;
 	const uint32_t cap = a.cap;
@@ -462,36 +558,45 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 	if (fits) {
 		// ---- phase 2: the whole segment into the arena, back to back -----
 #pragma unroll
-		for (uint32_t c = 0; c < RCH; c++) {
-			RPack p;
-			p.init(abit + base[c] + excl[c]);
-			pack_chunk(p, V[c], lp[c], k, s_tab);
-			p.flush();
-		}
-		if (wid == 0) {
-			uint2 pp = make_uint2(HDR_BITS, hdr_pred);
-			if (!is_first)
-				pp = rice_lookback(a, gseg, sif, lane);
-			if (lane == 0) {
-				if (!is_first)
-					gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (pp.x + A));
-				s_misc[0] = pp.x;
-				s_misc[1] = pp.y;
+		for (uint32_t c = 0; c <= RCH; c++) {
+			if (c == AIRS_RICE_LBC && wid == 0) {
+				// the look-back (wave 0), once this many chunks are packed
+				uint2 pp = make_uint2(HDR_BITS, hdr_pred);
+				dbg_stamp(a, gseg, 3);
+				if (DBG(2u)) // ablation: no look-back (offsets invented, output garbage)
+					pp = make_uint2(HDR_BITS + sif * 37u, 0u);
+				else if (!is_first)
+					pp = rice_lookback(a, gseg, sif, lane, gearly);
+				if (lane == 0) {
+					if (!is_first)
+						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (pp.x + A));
+					s_misc[0] = pp.x;
+					s_misc[1] = pp.y;
+				}
+				dbg_stamp(a, gseg, 2);
+			}
+			if (c < RCH && !(DBG(32u))) { // (ablation 32: no packing)
+				RPack p;
+				p.init(abit + base[c] + excl[c]);
+				pack_chunk(p, V[c], lp[c], k, s_tab);
+				p.flush();
 			}
 		}
 		__syncthreads(); // B2: arena complete, offset known
 		const uint32_t P = __builtin_amdgcn_readfirstlane(s_misc[0]);
 		const uint32_t pred = __builtin_amdgcn_readfirstlane(s_misc[1]);
-		rice_store(arena, P, A, pred, is_last, rsrc, fdst, cap, tid);
+		if (!(DBG(2048u))) // (ablation 2048: no stores)
+			rice_store(arena, P, A, pred, is_last, rsrc, fdst, cap, tid);
 		if (is_last && tid == 0)
 			s_misc[2] = P;
+		dbg_stamp(a, gseg, 4);
 	} else {
 		// ---- a segment that does not fit: offset first, then chunk by chunk
 		// through the arena (every chunk fits: 4096 x (k + 17) bits) --------
 		if (wid == 0) {
 			uint2 pp = make_uint2(HDR_BITS, hdr_pred);
 			if (!is_first)
-				pp = rice_lookback(a, gseg, sif, lane);
+				pp = rice_lookback(a, gseg, sif, lane, 0ull);
 			if (lane == 0) {
 				if (!is_first)
 					gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (pp.x + A));
@@ -522,7 +627,7 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 				pred = (pred << tot[c]) | (arena[0] >> (32u - tot[c]));
 			}
 			__syncthreads();
-			for (uint32_t i = tid; i < ((tot[c] + 31u) >> 5) + 1u; i += EWG)
+			for (uint32_t i = tid; i < ((tot[c] + 31u) >> 5) + 1u; i += RWG)
 				arena[i] = 0u;
 			__syncthreads();
 		}
@@ -566,6 +671,24 @@ __global__ __launch_bounds__(EWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		if (a.needed)
 			a.needed[frame] = size;
 	}
+	if (!PERSIST || dn >= a.num_segs)
+		break;
+	// every read of the arena is done: zero it for the next segment (its
+	// packing comes after the next B1)
+	__syncthreads();
+	{
+		uint4 *L4 = reinterpret_cast<uint4 *>(L_ar);
+		for (uint32_t i = tid; i < a.img_words / 4u; i += RWG)
+			L4[i] = make_uint4(0u, 0u, 0u, 0u);
+	}
+	d = dn;
+	sif = sif_n;
+	lf = lf_n;
+	gseg = lf * a.segs_per_frame + sif;
+	frame = frame_n;
+	fsrc = fsrc_n;
+	dbg_stamp(a, gseg, 0);
+	} // segments
 }
 
 // The launch, or false when it does not fit this kernel (the caller then
@@ -577,15 +700,40 @@ bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s)
 		return false;
 	if (k.frame_g || k.ktot || k.model_mode || !k.g || (k.g & (k.g - 1u)) || k.g > (1u << RICE_KMAX))
 		return false;
-	if (k.segs_per_frame == 0u || k.n != k.segs_per_frame * RSEGN)
+	if (k.segs_per_frame == 0u || k.n % RSEGN)
 		return false;
+	// this kernel's segments (RSEGN samples; the granule arrays hold one per
+	// AIRS_SEG-chunk segment of the caller, at least as many)
 	KArgs ka = k;
+	const uint32_t nfr = k.num_segs / k.segs_per_frame;
+	ka.segs_per_frame = k.n / RSEGN;
+	ka.num_segs = nfr * ka.segs_per_frame;
 	ka.img_words = rice_arena_words();
 	const size_t lds = (size_t)ka.img_words * 4u;
+#ifndef AIRS_RICE_PERSIST
+#define AIRS_RICE_PERSIST 0
+#endif
+	if (AIRS_RICE_PERSIST && !k.frame_list) {
+		// experiment: the resident grid walks the segments (no hole lists)
+		static int per_cu = 0, cus = 0;
+		if (!cus) {
+			int dev = 0;
+			(void)hipGetDevice(&dev);
+			(void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+			(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rice_kernel<PRE_DIFF, true>, RWG, lds);
+		}
+		uint32_t grid = (uint32_t)(per_cu * cus);
+		grid = grid < ka.num_segs ? grid : ka.num_segs;
+		if (pre == PRE_DIFF)
+			hipLaunchKernelGGL((rice_kernel<PRE_DIFF, true>), dim3(grid), dim3(RWG), lds, s, ka);
+		else
+			hipLaunchKernelGGL((rice_kernel<PRE_NONE, true>), dim3(grid), dim3(RWG), lds, s, ka);
+		return true;
+	}
 	if (pre == PRE_DIFF)
-		hipLaunchKernelGGL(rice_kernel<PRE_DIFF>, dim3(k.num_segs), dim3(EWG), lds, s, ka);
+		hipLaunchKernelGGL((rice_kernel<PRE_DIFF, false>), dim3(ka.num_segs), dim3(RWG), lds, s, ka);
 	else
-		hipLaunchKernelGGL(rice_kernel<PRE_NONE>, dim3(k.num_segs), dim3(EWG), lds, s, ka);
+		hipLaunchKernelGGL((rice_kernel<PRE_NONE, false>), dim3(ka.num_segs), dim3(RWG), lds, s, ka);
 	return true;
 }
 

@@ -55,14 +55,6 @@ uint32_t stream_segn(uint32_t sample_bytes)
 void stream_encode(const KArgs &k, uint32_t sample_bytes, uint32_t pre, uint32_t enc, bool rice, bool full,
 		   uint32_t grid, hipStream_t s)
 {
-	// the arena kernel's fast path (enc_arena.hip), as for frames
-	if (sample_bytes == 2 && (pre == PRE_NONE || pre == PRE_DIFF) && enc == ENC_ZERO && rice && full && k.g >= 1u &&
-	    k.g <= 2048u && arena_enabled()) {
-		KArgs ka = k;
-		ka.img_words = arena_words();
-		arena_encode(ka, pre, true, grid, s);
-		return;
-	}
 	if (sample_bytes == 2) {
 		if (pre == PRE_DIFF)
 			stream_enc<2, PRE_DIFF>(k, enc, rice, full, grid, s);

@@ -1314,274 +1314,51 @@ __global__ __launch_bounds__(1024) void walk_ctx_kernel(WArgs a)
 }
 
 // ---------------------------------------------------------------------
-// Frame walk with the per-frame Rice k (CMP_GPU_AUTO_RICE on 64 Ki-sample
-// 16-bit frames, BASELINE configs[2]): one 1024-thread workgroup codes whole
-// frames, workgroups strided over the launch's frames.  The encode kernel's
-// fused selection splits a frame over four workgroups, which must meet at
-// candidate granules (a round trip and five barriers before any packing);
-// here the frame never leaves the workgroup:
-//   * lane t holds samples [16t, 16t+16) of each of the 4 chunks in
-//     registers (32 VGPRs); each chunk's registers take the next frame's
-//     samples as soon as pass 2 has read them, so they land while this
-//     frame packs;
-//   * pass 1: residuals and the 129-bin histogram of v = m + 1 (per lane
-//     counters in image 0), bin totals, the 16 candidate
-//     sums and the argmin k (orc_select_rice_k's rule), all in the workgroup;
-//   * pass 2: the residuals again (from the registers), lengths with that k
-//     and the chunk packing of the context walk (cw_chunk: frame offsets are
-//     a running sum, no look-back), epilogue with g = 2^k.
-// ---------------------------------------------------------------------
-#define FA_CH 4u // chunks of CW_CHUNK samples per frame
-
-template <int PRE>
-__global__ __launch_bounds__(1024) void frame_auto_kernel(KArgs a)
-{
-	constexpr uint32_t RW = EPT * 2u / 16u; // uint4 per lane per chunk (16-bit samples)
-	extern __shared__ __attribute__((aligned(16))) uint32_t L_img[];
-	__shared__ uint32_t s_wsum[2][CW_WAVES];
-	__shared__ __attribute__((aligned(16))) uint2 s_tab[WTAB];
-	__shared__ uint32_t s_hist[AUTO_BINS];
-	__shared__ uint32_t s_kt[CW_WAVES][16];
-	__shared__ uint32_t s_k;
-
-	const uint32_t tid = threadIdx.x, lane = tid & 63u;
-	const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-	const uint32_t n = a.n; // FA_CH * CW_CHUNK
-	const uint32_t nfr = a.num_segs / a.segs_per_frame;
-	uint32_t *const img0 = L_img + 4, *const img1 = L_img + 4 + a.img_words;
-	for (uint32_t i = tid; i < 2u * a.img_words + 4u; i += CW_THREADS)
-		L_img[i] = 0u;
-
-	// this workgroup's frames: lf = blockIdx.x + i gridDim.x
-	auto frame_of = [&](uint32_t lf) {
-		return __builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
-	};
-	// chunk cc of frame lf into rs[cc]: issued once this frame's pass 2 has
-	// taken chunk cc from the registers, so the next frame's samples land
-	// while this one packs.  Unconditional (holes and the step past the last
-	// frame load frame 0 of the launch): see issue() in walk_ctx_kernel
-	uint4 rs[FA_CH][RW];
-	uint32_t pv[FA_CH];
-	auto load = [&](uint32_t cc, uint32_t lf) {
-		uint32_t fr = lf < nfr ? frame_of(lf) : AIRS_NO_FRAME;
-		fr = fr == AIRS_NO_FRAME ? frame_of(0u) : fr;
-		fr = fr == AIRS_NO_FRAME ? 0u : fr;
-		const uint8_t *fs = a.src + (uint64_t)fr * a.src_stride;
-		const uint32_t first = cc * CW_CHUNK + tid * EPT;
-		const uint4 *p = reinterpret_cast<const uint4 *>(fs + (size_t)first * 2u);
-#pragma unroll
-		for (uint32_t q = 0; q < RW; q++)
-			rs[cc][q] = p[q];
-		pv[cc] = PRE == PRE_DIFF ? (uint32_t)reinterpret_cast<const uint16_t *>(fs)[first ? first - 1u : 0u] : 0u;
-	};
-#pragma unroll
-	for (uint32_t cc = 0; cc < FA_CH; cc++)
-		load(cc, blockIdx.x);
-	// the histogram's per-lane counter of bin b: byte hbase + 256 (b + 1016)
-	// (encode_kernel's AUTO addressing; 32-bit LDS address arithmetic wraps)
-	const uint32_t hbase = (uint32_t)(uintptr_t)img0 + 4u * lane - 1016u * 256u;
-	const char *tab = reinterpret_cast<const char *>(s_tab);
-	CwState st;
-	st.used_prev = 0u;
-	__syncthreads(); // the zeroed images
-
-	for (uint32_t lf = blockIdx.x; lf < nfr; lf += gridDim.x) {
-		const uint32_t frame = frame_of(lf), nxt = lf + gridDim.x;
-		if (frame == AIRS_NO_FRAME) { // (uniform: the whole workgroup)
-#pragma unroll
-			for (uint32_t cc = 0; cc < FA_CH; cc++)
-				load(cc, nxt);
-			continue;
-		}
-
-		// ---- pass 1: residuals -> histogram of v = m + 1 ---------------------
-#pragma unroll
-		for (uint32_t cc = 0; cc < FA_CH; cc++) {
-			uint32_t w[EPT / 2], mp[EPT / 2];
-			cw_pairs<2>(rs[cc], 0u, w);
-			const uint32_t prevs = (cc != 0u || tid >= 64u) ? pv[cc] : 0u;
-			cw_primary<PRE, ENC_ZERO>(w, prevs, 0u, lane, mp);
-#pragma unroll
-			for (uint32_t jp = 0; jp < EPT / 2; jp++) {
-				uint32_t wv = mp[jp];
-				asm volatile("" : "+v"(wv));
-#pragma unroll
-				for (uint32_t h = 0; h < 2; h++) {
-					const uint32_t v = half16(wv, h) + 1u;
-					uint32_t ha;
-					asm("v_lshrrev_b32 %0, 20, %1\n\tv_lshl_add_u32 %0, %0, 8, %2"
-					    : "=&v"(ha)
-					    : "v"(__float_as_uint((float)v)), "v"(hbase));
-					__hip_atomic_fetch_add(reinterpret_cast<lds_u32 *>((uintptr_t)ha), 1u, __ATOMIC_RELAXED,
-							       __HIP_MEMORY_SCOPE_WORKGROUP);
-				}
-			}
-		}
-		__syncthreads();
-		// bin totals: 8 threads per row (two 16-byte reads each), row 128 by wave 0
-		{
-			uint32_t t8 = tid; // opaque: the hoisted addresses were spilled to scratch
-			asm volatile("" : "+v"(t8));
-			const uint32_t r = t8 >> 3, e = t8 & 7u;
-			const uint4 *row = reinterpret_cast<const uint4 *>(img0 + r * 64u + e * 8u);
-			const uint4 x = row[0], y = row[1];
-			uint32_t sm = x.x + x.y + x.z + x.w + y.x + y.y + y.z + y.w;
-			sm += __shfl_xor(sm, 1, 64);
-			sm += __shfl_xor(sm, 2, 64);
-			sm += __shfl_xor(sm, 4, 64);
-			if (e == 0u)
-				s_hist[r] = sm;
-			if (wid == 0u) {
-				const uint32_t s128 = wave_sum(img0[128u * 64u + lane]);
-				if (lane == 0u)
-					s_hist[128] = s128;
-			}
-		}
-		__syncthreads();
-		// the histogram rows back to zero (image 0 packs chunk 0; visible after
-		// cw_chunk's first barrier)
-		for (uint32_t i = tid; i < AUTO_BINS * 64u / 4u; i += CW_THREADS)
-			reinterpret_cast<uint4 *>(img0)[i] = make_uint4(0u, 0u, 0u, 0u);
-		// the 16 candidate sums: thread (slice sl, k) covers bins sl, sl + 64, sl + 128
-		{
-			const uint32_t k = tid & 15u, sl = tid >> 4;
-			uint32_t part = 0u;
-#pragma unroll
-			for (uint32_t i = 0; i < 3u; i++) {
-				const uint32_t b = sl + 64u * i;
-				if (b < AUTO_BINS)
-					part += s_hist[b] * auto_term(b, k);
-			}
-			part += __shfl_xor(part, 16, 64);
-			part += __shfl_xor(part, 32, 64);
-			if (lane < 16u)
-				s_kt[wid][k] = part;
-		}
-		__syncthreads();
-		if (wid == 0u) {
-			const uint32_t k = lane & 15u;
-			uint32_t tot = 0u;
-#pragma unroll
-			for (uint32_t wv = 0; wv < CW_WAVES; wv++)
-				tot += s_kt[wv][k];
-			// frame bits for k (< 2^28), ties to the smaller k (orc_select_rice_k)
-			uint32_t key = ((tot + n * (k + 1u)) << 4) | k;
-#pragma unroll
-			for (uint32_t d = 1; d < 16u; d <<= 1)
-				key = min(key, (uint32_t)__shfl_xor(key, d, 64));
-			if (lane == 0u)
-				s_k = key & 15u;
-		}
-		__syncthreads();
-		const uint32_t ks = __builtin_amdgcn_readfirstlane(s_k);
-		const Coder cd = make_coder<ENC_ZERO>(1u << ks, a.outlier_param);
-		const bool fast = ks <= 11u;
-		if (fast && tid < WTAB)
-			s_tab[tid] = walk_table_entry<ENC_ZERO>(tid, cd); // visible after cw_chunk's first barrier
-
-		// ---- pass 2: lengths with k, packing at the running frame offset ------
-		constexpr uint32_t HB = 176u; // NONE/DIFF + ZERO: the 22-byte header
-		st.P = HB;
-		st.carry = (cd.outlier & 0xFFFFu) << 16; // header bytes 20-21 share the first payload word
-		uint8_t *fdst = a.dst + (uint64_t)frame * a.dst_stride;
-		const u32x4 dst_rsrc = rsrc_words(fdst, a.cap & ~3u);
-#pragma unroll
-		for (uint32_t cc = 0; cc < FA_CH; cc++) {
-			uint4 r[RW];
-#pragma unroll
-			for (uint32_t q = 0; q < RW; q++) {
-				r[q] = rs[cc][q];
-				asm volatile("" : "+v"(r[q].x), "+v"(r[q].y), "+v"(r[q].z), "+v"(r[q].w));
-			}
-			uint32_t w[EPT / 2], mp[EPT / 2], oq[EPT / 2];
-			cw_pairs<2>(r, 0u, w);
-			const uint32_t prevs = (cc != 0u || tid >= 64u) ? pv[cc] : 0u;
-			load(cc, nxt); // the next frame's chunk cc
-			cw_primary<PRE, ENC_ZERO>(w, prevs, 0u, lane, mp);
-			const uint32_t T = walk_lengths<ENC_ZERO, true>(mp, oq, cd, fast, tab);
-#pragma unroll
-			for (uint32_t q = 0; q < EPT / 2; q++)
-				asm volatile("" : "+v"(mp[q]), "+v"(oq[q]));
-			uint32_t *const img = (cc & 1u) ? img1 : img0;
-			uint32_t *const imgo = (cc & 1u) ? img0 : img1;
-			cw_chunk<ENC_ZERO, true>(st, img, imgo, s_wsum, cc & 1u, T, mp, oq, cd, fast, tab, dst_rsrc);
-		}
-		if (tid == 0u) {
-			const uint32_t size = ((st.P + 7u) >> 3) + (a.checksum ? 4u : 0u);
-			const uint64_t id = a.ids ? a.ids[lf] : a.id_base + (uint64_t)lf * a.id_step;
-			uint32_t h[5];
-			header_words(h, size, 2u * n, id, a.seqs ? a.seqs[frame] : a.seq, PRE, a.checksum ? 1u : 0u, ENC_ZERO,
-				     0u, cd.g, cd.outlier);
-			cw_epilogue(fdst, a.cap, st.P, st.carry, HB, a.checksum != 0u, a.checksum ? a.checksums[frame] : 0u, h,
-				    a.status, a.needed, frame, size);
-		}
-	}
-}
-
-// launches frame_auto_kernel when the launch fits it: 16-bit samples, frames
-// of FA_CH * CW_CHUNK samples (16-byte aligned: FULL); false otherwise
-bool frame_auto_encode(const KArgs &k, uint32_t pre, hipStream_t s)
-{
-	if (k.n != FA_CH * CW_CHUNK || (pre != PRE_NONE && pre != PRE_DIFF))
-		return false;
-	KArgs ka = k;
-	// k up to 15: 32-bit codewords at most (the escape at k = 15), plus flush words
-	ka.img_words = CW_CHUNK + 8u;
-	const size_t lds = (size_t)(2u * ka.img_words + 4u) * 4u;
-	const uint32_t nfr = k.num_segs / k.segs_per_frame;
-	// one workgroup per CU (1024 threads, ~129 KiB of LDS), strided over the frames
-	int dev = 0, cus = 256;
-	if (hipGetDevice(&dev) == hipSuccess)
-		(void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-	const uint32_t grid = nfr < (uint32_t)cus ? nfr : (uint32_t)cus;
-	if (pre == PRE_DIFF)
-		hipLaunchKernelGGL(frame_auto_kernel<PRE_DIFF>, dim3(grid), dim3(CW_THREADS), lds, s, ka);
-	else
-		hipLaunchKernelGGL(frame_auto_kernel<PRE_NONE>, dim3(grid), dim3(CW_THREADS), lds, s, ka);
-	return true;
-}
-
-// ---------------------------------------------------------------------
 // launch (airs_dev_walk, airs_dev.h)
 // ---------------------------------------------------------------------
 // the segment walk's launch: the block index is the logical index when the
 // whole grid is resident at once (occupancy of this kernel x CUs), else a ticket
+//
+// Direct launches assume that every workgroup of the grid is running, so a
+// look-back only ever waits on a running workgroup.  That holds only when
+// nothing else occupies the device: the engine must be marked exclusive
+// (CMP_GPU_OPT_EXCLUSIVE), and the grid must fit what the CUs admit.  The
+// occupancy API reads one block per CU high at some SGPR counts
+// (MI355X_MICROARCH.md "Residency"), so the count is also capped by the
+// guide's SGPR rule at the largest allocation a kernel can have (102 SGPRs +
+// VCC: 112 per wave, 800 per SIMD: 6 waves per SIMD).  Otherwise each
+// workgroup takes its logical index from the ticket counter as it starts.
 template <typename K>
-static int walk_go(K kern, const WArgs &k, size_t lds, hipStream_t s)
+static int walk_go(K kern, const WArgs &k, size_t lds, hipStream_t s, bool exclusive)
 {
 	const uint32_t grid = k.num_ctx * k.spf;
-	static int cus = 0;
-	if (!cus) {
-		int dev = 0;
-		if (hipGetDevice(&dev) != hipSuccess ||
-		    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-			cus = -1;
-	}
-	int per_cu = 0;
+	int dev = 0, cus = 0, per_cu = 0;
+	if (hipGetDevice(&dev) != hipSuccess ||
+	    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+		cus = 0;
 	if (cus > 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 320, lds) != hipSuccess)
 		per_cu = 0;
 	WArgs kk = k;
-	kk.direct = (cus > 0 && per_cu > 0 && (uint64_t)grid <= (uint64_t)per_cu * (uint64_t)cus) ? 1u : 0u;
+	const int sgpr_cap = 4 * (800 / (112 + 16)) / 5; // 320-thread (5-wave) blocks per CU
+	per_cu = per_cu < sgpr_cap ? per_cu : sgpr_cap;
+	kk.direct =
+		(exclusive && cus > 0 && per_cu > 0 && (uint64_t)grid <= (uint64_t)per_cu * (uint64_t)cus) ? 1u : 0u;
 	kk.cus = cus > 0 ? (uint32_t)cus : 0u;
-	if (const char *e = getenv("AIRS_WALK_PRIO")) // A/B: 0 leaves every workgroup at priority 0
-		kk.cus = atoi(e) ? kk.cus : 0u;
-	if (const char *e = getenv("AIRS_WALK_TICKET")) // tests: 1 forces the ticket
-		kk.direct = atoi(e) ? 0u : kk.direct;
 	hipLaunchKernelGGL(kern, dim3(grid), dim3(320), lds, s, kk);
 	return kk.direct ? 1 : 0;
 }
 
 // < 0: no kernel for these passes; 0: launched with the ticket; 1: direct
 template <int W, int PRE_P, int ENC_P, bool RICE_P>
-static int walk_launch_s(const WArgs &k, uint32_t enc_s, bool rice_s, size_t lds, hipStream_t s)
+static int walk_launch_s(const WArgs &k, uint32_t enc_s, bool rice_s, size_t lds, hipStream_t s, bool ex)
 {
 	const bool half = k.spf * walk_seg_samples(true) == k.n && k.spf * walk_seg_samples(false) != k.n;
 	if (enc_s == ENC_ZERO && rice_s)
-		return half ? walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 8>, k, lds, s)
-			    : walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 16>, k, lds, s);
+		return half ? walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 8>, k, lds, s, ex)
+			    : walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_ZERO, true, 16>, k, lds, s, ex);
 	if (enc_s == ENC_MULTI && rice_s)
-		return half ? walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 8>, k, lds, s)
-			    : walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 16>, k, lds, s);
+		return half ? walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 8>, k, lds, s, ex)
+			    : walk_go(walk_kernel<W, PRE_P, ENC_P, RICE_P, ENC_MULTI, true, 16>, k, lds, s, ex);
 	return -1;
 }
 
@@ -1593,12 +1370,12 @@ uint32_t walk_seg_samples(bool half)
 
 template <int W, int PRE_P>
 static int walk_launch_p(const WArgs &k, uint32_t enc_p, bool rice_p, uint32_t enc_s, bool rice_s, size_t lds,
-			 hipStream_t s)
+			 hipStream_t s, bool ex)
 {
 	if (enc_p == ENC_ZERO && rice_p)
-		return walk_launch_s<W, PRE_P, ENC_ZERO, true>(k, enc_s, rice_s, lds, s);
+		return walk_launch_s<W, PRE_P, ENC_ZERO, true>(k, enc_s, rice_s, lds, s, ex);
 	if (enc_p == ENC_MULTI && rice_p)
-		return walk_launch_s<W, PRE_P, ENC_MULTI, true>(k, enc_s, rice_s, lds, s);
+		return walk_launch_s<W, PRE_P, ENC_MULTI, true>(k, enc_s, rice_s, lds, s, ex);
 	return -1;
 }
 
@@ -1646,16 +1423,16 @@ bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint
 }
 
 int walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
-		bool rice_s, hipStream_t s)
+		bool rice_s, hipStream_t s, bool exclusive)
 {
 	// walk_kernel's images, then the deferred frame epilogues
 	const size_t lds = (size_t)(AIRS_WALK_NIMG * (k.img_words + 4u) + 4u) * 4u +
 			   (k.fpc <= AIRS_WALK_EPI_MAX ? (size_t)k.fpc * 16u : 0u);
 	if (sample_bytes == 2)
-		return pre_p == PRE_DIFF ? walk_launch_p<2, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
-					 : walk_launch_p<2, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);
-	return pre_p == PRE_DIFF ? walk_launch_p<4, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
-				 : walk_launch_p<4, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);
+		return pre_p == PRE_DIFF ? walk_launch_p<2, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s, exclusive)
+					 : walk_launch_p<2, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s, exclusive);
+	return pre_p == PRE_DIFF ? walk_launch_p<4, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s, exclusive)
+				 : walk_launch_p<4, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s, exclusive);
 }
 
 } // namespace airs

@@ -981,7 +981,32 @@ struct airs_dev_engine {
 	size_t rhist_cap; // frames
 	void *pinned; // page-locked host scratch (read-backs, identifier uploads)
 	size_t pinned_cap;
+	// cmp_gpu_engine_set_option (include/cmp_gpu.h)
+	uint32_t opt_exclusive;     // CMP_GPU_OPT_EXCLUSIVE
+	uint32_t opt_walk_segment;  // CMP_GPU_OPT_WALK_SEGMENT: 0, 2048 or 4096
+	uint32_t opt_no_ctx_walk;   // CMP_GPU_OPT_NO_CONTEXT_WALK
 };
+
+extern "C" uint32_t airs_dev_set_option(struct airs_dev_engine *e, uint32_t option, uint32_t value)
+{
+	if (!e)
+		return ERRV(E_GENERIC);
+	switch (option) {
+	case AIRS_OPT_EXCLUSIVE:
+		e->opt_exclusive = value ? 1u : 0u;
+		return 0;
+	case AIRS_OPT_WALK_SEGMENT:
+		if (value != 0u && value != 2048u && value != 4096u)
+			return ERRV(E_PARAMS_INVALID);
+		e->opt_walk_segment = value;
+		return 0;
+	case AIRS_OPT_NO_CONTEXT_WALK:
+		e->opt_no_ctx_walk = value ? 1u : 0u;
+		return 0;
+	default:
+		return ERRV(E_PARAMS_INVALID);
+	}
+}
 
 extern "C" int airs_dev_available(void)
 {
@@ -1154,30 +1179,10 @@ static uint32_t ensure_granules(airs_dev_engine *e, size_t segs)
 	return 0;
 }
 
-// AIRS_FAUTO=1 (env, read at each launch: A/B and tests) sends AUTO launches
-// of 64 Ki-sample frames to the frame walk (frame_auto_kernel); measured
-// slower than the fused encode kernel on cfg3 (78.7 against 75.0 us,
-// DESIGN.md 3.1.1), so off by default
-static bool fauto_enabled()
-{
-	const char *e = getenv("AIRS_FAUTO");
-	return e ? atoi(e) != 0 : false;
-}
-
 template <int W, int PRE, int ENC, bool RICE, int MODEL>
 static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t s)
 {
 	if constexpr (ENC == ENC_ZERO && RICE && MODEL == 0 && (PRE == PRE_NONE || PRE == PRE_DIFF)) {
-		// the frame walk (64 Ki-sample frames: one workgroup per frame, no
-		// candidate granules; opt-in, AIRS_FAUTO=1)
-		if (k.ktot && W == 2 && full && fauto_enabled() && frame_auto_encode(k, PRE, s))
-			return;
-		if (k.ktot && W == 2 && full && arena_auto_enabled()) { // fused Rice selection, the arena kernel
-			KArgs ka = k;
-			ka.img_words = arena_words();
-			arena_auto_encode(ka, PRE, grid, s);
-			return;
-		}
 		if (k.ktot) { // fused per-frame Rice selection (frame barrier: never persistent)
 			size_t lds = (size_t)2u * (k.img_words + 4u) * 4u; // two images (enc_kernel.h NIMG)
 			lds = lds > AUTO_BINS * 64u * 4u ? lds : AUTO_BINS * 64u * 4u; // the histogram
@@ -1196,16 +1201,6 @@ static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t 
 		      MODEL == 0) {
 		if (full && rice_encode(k, PRE, s))
 			return;
-	}
-	// the arena kernel (enc_arena.hip): 16-bit NONE/DIFF, Rice ZERO with
-	// k <= 11 for every frame, no model, whole aligned segments
-	if constexpr (W == 2 && (PRE == PRE_NONE || PRE == PRE_DIFF) && ENC == ENC_ZERO && RICE && MODEL == 0) {
-		if (full && !k.frame_g && k.g >= 1u && k.g <= 2048u && arena_enabled()) {
-			KArgs ka = k;
-			ka.img_words = arena_words();
-			arena_encode(ka, PRE, false, grid, s);
-			return;
-		}
 	}
 	const size_t lds = (size_t)seg_images(W, MODEL) * (k.img_words + 4u) * 4u;
 #ifdef AIRS_EXP_ONLY
@@ -1517,15 +1512,16 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 // words of ONE of the context walk's two images (16384 samples of the
 // longer-coded pass), or 0 when the batch does not take the context walk:
 // frames of its size, enough contexts to fill the CUs, two images in the LDS
-static uint32_t ctx_walk_words(const struct airs_walk *w)
+// (no_ctx: the engine's CMP_GPU_OPT_NO_CONTEXT_WALK; batches with the
+// fallback on the chip need the context walk and ignore it)
+static uint32_t ctx_walk_words(const struct airs_walk *w, bool no_ctx)
 {
 	const uint32_t mbp = code_max_bits(w->enc_p, w->g_p, w->outl_p);
 	const uint32_t mbs = code_max_bits(w->enc_s, w->g_s, w->outl_s);
 	const uint32_t mb = mbp > mbs ? mbp : mbs;
 	const uint32_t cw = ((walk_ctx_samples() / 4u * mb / 32u + 8u) + 3u) & ~3u;
-	if (const char *e = getenv("AIRS_WALK_CTX")) // A/B: 0 sends these batches to the segment walk
-		if (!atoi(e) && !w->fb)
-			return 0u;
+	if (no_ctx && !w->fb)
+		return 0u;
 	if (w->n == walk_ctx_samples() && w->num_ctx >= AIRS_WALK_CTX_MIN && (2u * cw + 4u) * 4u <= 150u * 1024u)
 		return cw;
 	return 0u;
@@ -1543,7 +1539,7 @@ extern "C" int airs_dev_walk_supported(const struct airs_walk *w)
 	if (!w->model_ptrs && (((uintptr_t)w->model & 15u) || (w->model_stride & 15u)))
 		return 0;
 	if (w->fb && (!w->draws || !w->seq_out || w->cap != w->raw_size || w->raw_size < 16u + 2u * w->n ||
-		      !ctx_walk_words(w)))
+		      !ctx_walk_words(w, false)))
 		return 0;
 	const uint64_t segs = (uint64_t)w->num_ctx * (w->n / AIRS_SEG);
 	return segs <= 0x7FFFFFFFull && segs * w->fpc <= 0x7FFFFFFFull;
@@ -1557,8 +1553,8 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 	// the segment walk takes 2048-sample segments when 4096-sample ones would
 	// leave fewer than four workgroups per CU (AIRS_WALK_HALF_BELOW)
 	bool half = (uint64_t)w->num_ctx * (w->n / AIRS_SEG) < AIRS_WALK_HALF_BELOW;
-	if (const char *sg = getenv("AIRS_WALK_SEG")) // tests and A/B: 2048 or 4096 forces the segment size
-		half = atoi(sg) == 2048 ? true : atoi(sg) == 4096 ? false : half;
+	if (e->opt_walk_segment) // CMP_GPU_OPT_WALK_SEGMENT forces the segment size
+		half = e->opt_walk_segment == 2048u;
 	const uint32_t spf = w->n / walk_seg_samples(half);
 	const uint64_t total = (uint64_t)w->num_ctx * w->fpc;
 	uint32_t r = ensure_granules(e, (size_t)(total * spf));
@@ -1613,7 +1609,7 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 	// one context per workgroup when the frames have its size, there are
 	// enough contexts to fill the CUs, and two images fit the LDS
 	{
-		const uint32_t cw = ctx_walk_words(w);
+		const uint32_t cw = ctx_walk_words(w, e->opt_no_ctx_walk != 0u);
 		if (cw) {
 			WArgs kc = k;
 			kc.img_words = cw;
@@ -1641,7 +1637,8 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 	}
 #endif
 	k.ticket_base = e->walk_ticket_base;
-	const int wr = walk_encode(k, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream);
+	const int wr = walk_encode(k, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream,
+				   e->opt_exclusive != 0u);
 	if (wr < 0)
 		return ERRV(E_PARAMS_INVALID);
 	HIPCHECK(hipGetLastError());

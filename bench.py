@@ -378,6 +378,10 @@ def main():
     assert lib.gpu_available(), "no HIP device"
     stream = torch.cuda.current_stream()
     eng = lib.engine(stream.cuda_stream)
+    # this process owns its GPU for the run (one rank per GPU, nothing else on
+    # the device while the timed kernels run): the MODEL segment walk may order
+    # its workgroups by block index (include/cmp_gpu.h CMP_GPU_OPT_EXCLUSIVE)
+    assert eng.set_option(pkg.OPT_EXCLUSIVE, 1) == 0
 
     wname = args.workload or ("cfg2" if world == 1 else "cfg4")
     wl = WORKLOADS[wname]
@@ -521,28 +525,21 @@ def main():
     ms_step = wall_max / args.steps * 1e3
     traffic, traffic_src = measured_traffic(wname)
     achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
-    ctl = os.environ.get("AIRS_ARENA_CTL", "0") not in ("", "0")
-    arena = ("airs::arena_kernel<DIFF,%s,%s> (enc_arena.hip: the Rice/ZERO fast path, one LDS arena per 16 Ki-sample "
-             "segment%s)" % ("STREAM" if wname == "cfg2s" else "frames", "CTL" if ctl else "-",
-                             ", a control wave runs the look-back" if ctl else ""))
-    if os.environ.get("AIRS_ARENA", "0") in ("", "0"):  # the arena kernel is opt-in
-        arena = ("airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL> (enc_kernel.h: 16 Ki-sample segments, decoupled "
-                 "look-back)")
+    rice = ("airs::rice_kernel<DIFF> (enc_rice.hip: 16 Ki-sample segments, codeword pairs from phase 1, one LDS "
+            "arena per segment, decoupled look-back)")
     kernels = {
-        "cfg2": arena + ": one launch per step",
-        "cfg2s": arena + ": one launch per step, one look-back chain of 4096 segments",
-        "cfg3": ("airs::frame_auto_kernel<DIFF> (enc_walk.hip: one 1024-thread workgroup per 64 Ki-sample frame, "
-                 "strided; the frame's Rice k from a histogram of the samples in registers, no granules)"
-                 if os.environ.get("AIRS_FAUTO", "0") not in ("", "0") else
-                 "airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO> (the per-frame Rice k chosen in-kernel from a "
-                 "histogram of the samples in registers)") + ": one launch per step",
-        "cfg4": arena + ": one launch per step",
+        "cfg2": rice + ": one launch per step",
+        "cfg2s": ("airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,-,STREAM> (enc_kernel.h: 16 Ki-sample segments): "
+                  "one launch per step, one look-back chain of 4096 segments"),
+        "cfg3": ("airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO> (the per-frame Rice k chosen in-kernel from a "
+                 "histogram of the samples in registers): one launch per step"),
+        "cfg4": rice + ": one launch per step",
         "cfg5": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> (enc_walk.hip): ONE launch per step, one "
                 "1024-thread workgroup per stream walks its 16 acquisitions, the model in registers",
         "cfg5s8": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,%d> (enc_walk.hip, the segment walk): ONE launch "
                   "per step, a 320-thread workgroup per (stream, %d-sample segment) walks the 16 acquisitions, each "
                   "acquisition's look-back resolved one step later" %
-                  ((16, 4096) if os.environ.get("AIRS_WALK_SEG") == "4096" else (8, 2048)),
+                  (8, 2048),
         "cfg5fb": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> with the uncompressed fallback resolved on "
                   "the chip: ONE launch per step, then one read-back of the draw counts and the identifier patch "
                   "(patch_ids_kernel)",

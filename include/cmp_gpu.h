@@ -79,6 +79,26 @@ struct cmp_gpu_engine;
 uint32_t cmp_gpu_engine_create(struct cmp_gpu_engine **engine, void *hip_stream);
 void cmp_gpu_engine_destroy(struct cmp_gpu_engine *engine);
 
+/* Engine options, all 0 after cmp_gpu_engine_create.  Returns 0 or an error
+ * value (CMP_ERROR(PARAMS_INVALID) for an unknown option or value).
+ *   CMP_GPU_OPT_EXCLUSIVE       1: the caller promises that nothing else runs
+ *                               on the device while this engine's kernels do
+ *                               (one process, one stream).  The MODEL segment
+ *                               walk may then order its workgroups by block
+ *                               index when its whole grid fits the CUs; without
+ *                               it every workgroup numbers itself with a
+ *                               ticket as it starts, which stays correct beside
+ *                               other kernels and processes.
+ *   CMP_GPU_OPT_WALK_SEGMENT    MODEL segment walk: 0 automatic, or 2048 /
+ *                               4096 samples per segment.
+ *   CMP_GPU_OPT_NO_CONTEXT_WALK 1: MODEL batches take the segment walk where
+ *                               they would take the context walk (not those
+ *                               with the uncompressed fallback, which need it). */
+#define CMP_GPU_OPT_EXCLUSIVE 1u
+#define CMP_GPU_OPT_WALK_SEGMENT 2u
+#define CMP_GPU_OPT_NO_CONTEXT_WALK 3u
+uint32_t cmp_gpu_engine_set_option(struct cmp_gpu_engine *engine, uint32_t option, uint32_t value);
+
 /* Compress num_ctx * frames_per_ctx frames (see the ordering note above).
  * Returns CMP_ERR_NO_ERROR or a call-level error (batch validation: NULL or
  * misaligned pointers, bad sizes, invalid contexts).  Per-frame results,

@@ -11,7 +11,6 @@ $H -c csrc/encode.hip -o ../exp/$n/encode.o &
 $H -c csrc/enc_stream.hip -o ../exp/$n/enc_stream.o &
 $H -c csrc/enc_rice.hip -o ../exp/$n/enc_rice.o &
 $H -c csrc/enc_walk.hip -o ../exp/$n/enc_walk.o &
-$H -c csrc/enc_arena.hip -o ../exp/$n/enc_arena.o &
 wait
-/opt/rocm/bin/hipcc -shared -Wl,-Bsymbolic -Wl,--no-undefined ../exp/$n/encode.o ../exp/$n/enc_rice.o ../exp/$n/enc_stream.o ../exp/$n/enc_walk.o ../exp/$n/enc_arena.o build/decode.o build/cmp_host.o -o ../exp/$n/libairscmp.so
-rm -f ../exp/$n/encode.o ../exp/$n/enc_rice.o ../exp/$n/enc_stream.o ../exp/$n/enc_walk.o ../exp/$n/enc_arena.o
+/opt/rocm/bin/hipcc -shared -Wl,-Bsymbolic -Wl,--no-undefined ../exp/$n/encode.o ../exp/$n/enc_rice.o ../exp/$n/enc_stream.o ../exp/$n/enc_walk.o build/decode.o build/cmp_host.o -o ../exp/$n/libairscmp.so
+rm -f ../exp/$n/encode.o ../exp/$n/enc_rice.o ../exp/$n/enc_stream.o ../exp/$n/enc_walk.o

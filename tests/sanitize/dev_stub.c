@@ -50,6 +50,16 @@ struct airs_dev_engine *airs_dev_engine_create(void *stream)
 	return calloc(1, sizeof(struct airs_dev_engine));
 }
 
+uint32_t airs_dev_set_option(struct airs_dev_engine *e, uint32_t option, uint32_t value)
+{
+	if (!e)
+		return (uint32_t)0 - 1u;
+	if (option < AIRS_OPT_EXCLUSIVE || option > AIRS_OPT_NO_CONTEXT_WALK)
+		return (uint32_t)0 - 10u;
+	(void)value;
+	return 0;
+}
+
 void airs_dev_engine_destroy(struct airs_dev_engine *e)
 {
 	if (!e)

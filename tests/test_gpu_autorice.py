@@ -139,44 +139,6 @@ def test_autorice_vs_oracle(prod, eng, orc, orc_ext, kind, pre, n):
                      f"{[(api.parse_header(got[f])['encoder_param'], api.parse_header(want[f])['encoder_param']) for f in bad[:4]]}")
 
 
-ARENA_CASES = [("u16", 1, SEG16), ("i16", 0, 4 * SEG16), ("u16", 0, AUTO_MAX_SPF * SEG16), ("u16", 1, 4 << 20)]
-
-
-@pytest.mark.parametrize("kind,pre,n", ARENA_CASES)
-def test_autorice_arena_vs_oracle(prod, eng, orc, orc_ext, monkeypatch, kind, pre, n):
-    """The same cases through the arena kernel's fused selection (an
-    experiment, off by default: AIRS_ARENA=1, read at each launch)."""
-    monkeypatch.setenv("AIRS_ARENA", "1")
-    test_autorice_vs_oracle(prod, eng, orc, orc_ext, kind, pre, n)
-
-
-FRAME_WALK_CASES = [("u16", 1, 300, 0), ("i16", 0, 300, 1), ("u16", 0, 40, 1), ("i16", 1, 40, 0)]
-
-
-@pytest.mark.parametrize("kind,pre,nf,checksum", FRAME_WALK_CASES)
-def test_autorice_frame_walk_vs_oracle(prod, eng, orc, orc_ext, monkeypatch, kind, pre, nf, checksum):
-    """64 Ki-sample 16-bit frames through the frame walk (frame_auto_kernel, an
-    experiment, opt-in with AIRS_FAUTO=1: measured slower than the fused
-    encode kernel; one workgroup per frame, strided; 300 frames: workgroups code several frames,
-    the next frame's samples loaded while one packs): frames of every scale
-    (k = 0 .. 15), the extreme value 65535, checksums; bit-exact against the
-    oracle's rule and encoder, and equal to the fused encode kernel's frames
-    (AIRS_FAUTO=0)."""
-    rng = np.random.default_rng(zlib.crc32(f"fw/{kind}/{pre}/{nf}".encode()))
-    frames = _frames(rng, kind, 4 * SEG16, nf, extreme=True)
-    want = _oracle(orc, orc_ext, kind, pre, frames, checksum)
-    monkeypatch.setenv("AIRS_FAUTO", "1")
-    got = _gpu(prod, eng, kind, pre, frames, checksum)
-    bad = [f for f in range(nf) if _mask(got[f]) != _mask(want[f])]
-    assert not bad, (f"frames {bad[:8]} differ; g gpu/oracle "
-                     f"{[(api.parse_header(got[f])['encoder_param'], api.parse_header(want[f])['encoder_param']) for f in bad[:4]]}")
-    ks = {api.parse_header(g)["encoder_param"].bit_length() - 1 for g in got}
-    assert nf < 100 or len(ks) >= 12, sorted(ks)
-    monkeypatch.setenv("AIRS_FAUTO", "0")
-    fused = _gpu(prod, eng, kind, pre, frames, checksum)
-    assert [_mask(g) for g in fused] == [_mask(g) for g in got]
-
-
 def test_autorice_k_range(prod, eng, orc, orc_ext):
     """The sweep reaches every k: scales 2^-1 .. 2^15.5 over 64 frames."""
     rng = np.random.default_rng(11)

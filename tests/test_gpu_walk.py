@@ -24,7 +24,8 @@ import pytest
 from conftest import load_pkg
 
 pytestmark = pytest.mark.gpu
-api = load_pkg().cmpapi
+pkg = load_pkg()
+api = pkg.cmpapi
 P = api.CmpParams
 RICE = (1, 2, 4, 8, 16, 32, 64, 1024, 32768)
 
@@ -36,6 +37,15 @@ def eng(prod):
     e = prod.engine()
     yield e
     e.close()
+
+
+@pytest.fixture(autouse=True)
+def _engine_options(eng):
+    """Engine options (cmp_gpu_engine_set_option) are per engine: every test
+    leaves the module's engine at the defaults."""
+    yield
+    eng.set_option(pkg.OPT_WALK_SEGMENT, 0)
+    eng.set_option(pkg.OPT_EXCLUSIVE, 0)
 
 
 def _ts_counter(start):
@@ -165,12 +175,14 @@ def make_case(trial):
     return params, kind, n, nctx, calls, cap
 
 
-@pytest.mark.parametrize("block,seg", [(b, None) for b in range(6)] + [(b, "4096") for b in range(3)])
-def test_walk_vs_call_loop(prod, eng, orc, monkeypatch, block, seg):
+@pytest.mark.parametrize("block,seg,excl", [(b, None, b % 2) for b in range(6)] + [(b, "4096", b % 2) for b in range(3)])
+def test_walk_vs_call_loop(prod, eng, orc, block, seg, excl):
     """seg: these few-context batches take 2048-sample segments (8 samples per
-    lane); AIRS_WALK_SEG=4096 forces the 16-sample form on the same trials."""
-    if seg:
-        monkeypatch.setenv("AIRS_WALK_SEG", seg)
+    lane); CMP_GPU_OPT_WALK_SEGMENT 4096 forces the 16-sample form on the same
+    trials.  excl: CMP_GPU_OPT_EXCLUSIVE, under which grids that fit the CUs
+    order their workgroups by block index instead of a ticket."""
+    assert eng.set_option(pkg.OPT_WALK_SEGMENT, int(seg) if seg else 0) == 0
+    assert eng.set_option(pkg.OPT_EXCLUSIVE, excl) == 0
     bad = []
     for trial in range(block * 12, block * 12 + 12):
         params, kind, n, nctx, calls, cap = make_case(trial)
@@ -259,16 +271,17 @@ CTX_CASES = [  # (kind, pre_p, enc_p, g_p, o_p, enc_s, g_s, o_s, iters, rate, ch
 
 @pytest.mark.parametrize("case,nctx,seg", [(c, 128, None) for c in range(len(CTX_CASES))] +
                          [(0, 32, None), (4, 32, None), (0, 32, "4096"), (2, 32, None)])
-def test_walk_ctx_vs_call_loop(prod, eng, orc, monkeypatch, case, nctx, seg):
+def test_walk_ctx_vs_call_loop(prod, eng, orc, case, nctx, seg):
     """Batches of >= 128 contexts of 64 Ki-sample frames take the context walk
     (one workgroup per context, walk_ctx_kernel); 32 contexts (configs[4]'s
     per-GPU share at N = 8) take the segment walk (walk_kernel, each
     acquisition's look-back one step late; 2048-sample segments, or 4096 with
-    AIRS_WALK_SEG).  Frames, sizes, context states and work buffers equal the
+    CMP_GPU_OPT_WALK_SEGMENT).  Frames, sizes, context states and work buffers equal the
     call loop; two calls in a row, so the second starts mid-sequence with the
     model read back from the work buffers."""
     if seg:
-        monkeypatch.setenv("AIRS_WALK_SEG", seg)
+        assert eng.set_option(pkg.OPT_WALK_SEGMENT, int(seg)) == 0
+    eng.set_option(pkg.OPT_EXCLUSIVE, 1 if nctx == 32 and case == 0 else 0)
     kind, pre, ep, gp, op, es, gs, osx, iters, rate, ck = CTX_CASES[case]
     rng = np.random.default_rng(500 + case + nctx)
     n = 65536
@@ -345,7 +358,7 @@ def test_whole_unit_frames_vs_call_loop(prod, eng, orc, case):
 
 
 @pytest.mark.parametrize("seg", [None, "2048"])
-def test_segment_walk_more_workgroups_than_resident(prod, eng, orc, monkeypatch, seg):
+def test_segment_walk_more_workgroups_than_resident(prod, eng, orc, seg):
     """a segment walk whose grid exceeds what the GPU holds at once
     (1100 contexts x one 4096-sample segment, 320-thread workgroups with two
     images each: at most 1024 resident; or x two 2048-sample segments, 2200
@@ -353,7 +366,8 @@ def test_segment_walk_more_workgroups_than_resident(prod, eng, orc, monkeypatch,
     workgroups take logical indices from a ticket, so a look-back only waits
     on a running workgroup; no give-up, frames and state equal the call loop."""
     if seg:
-        monkeypatch.setenv("AIRS_WALK_SEG", seg)
+        assert eng.set_option(pkg.OPT_WALK_SEGMENT, int(seg)) == 0
+    eng.set_option(pkg.OPT_EXCLUSIVE, 1)  # too many workgroups for the direct form: the ticket anyway
     rng = np.random.default_rng(31)
     kind, n, nctx, fpc = "u16", 4096, 1100, 12
     p = P(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16, secondary_iterations=15,
@@ -367,3 +381,44 @@ def test_segment_walk_more_workgroups_than_resident(prod, eng, orc, monkeypatch,
     bad = [f for f in range(len(fw)) if fw[f] != fg[f]]
     assert not bad, f"frames {bad[:8]} differ"
     assert sw == sg
+
+
+def test_segment_walk_beside_other_kernels(prod, eng, orc, orc_ext):
+    """a cfg5s8-shaped segment walk (configs[4]'s parameters, 32
+    streams x 16 acquisitions x 64 Ki i16-in-i32 samples, 1024 workgroups)
+    while kernels on a second stream keep the CUs busy.  The engine is not
+    marked exclusive, so every workgroup numbers itself with a ticket as it
+    starts and a look-back only waits on a running workgroup: bit-exact
+    frames and state against the call loop, no look-back give-up
+    (CMP_ERR_INT_BITSTREAM from cmp_gpu_synchronize)."""
+    import threading
+
+    import torch
+    n, nctx, fpc = 65536, 32, 16
+    srcs = []
+    for f in range(nctx * fpc):
+        x = np.empty(n, dtype=np.int32)
+        orc_ext.orc_synth_i32(0xA1A9, f, n, 32, x.ctypes.data)
+        srcs.append(x)
+    p = P(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16, secondary_iterations=15,
+          secondary_preprocessing=3, secondary_encoder_type=2, secondary_encoder_param=8,
+          secondary_encoder_outlier=107, model_rate=11)
+    cap = 26 + 6 * n
+    want = run_host(orc, [p] * nctx, "i16_in_i32", n, nctx, [(fpc, srcs)], cap)
+    side = torch.cuda.Stream()
+    buf = torch.empty(1 << 27, dtype=torch.float32, device="cuda")  # 512 MiB of elementwise work per op
+    stop = threading.Event()
+
+    def load():
+        with torch.cuda.stream(side):
+            while not stop.is_set():
+                buf.mul_(1.0001).add_(0.5)
+                side.synchronize()
+    t = threading.Thread(target=load)
+    t.start()
+    try:
+        got = run_gpu(prod, eng, [p] * nctx, "i16_in_i32", n, nctx, [(fpc, srcs)], cap)
+    finally:
+        stop.set()
+        t.join()
+    assert got == want

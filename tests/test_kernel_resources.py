@@ -19,20 +19,15 @@ LIB = os.path.join(PKG_DIR, "lib", "libairscmp.so")
 
 # symbol: (max VGPRs, max SGPR spills to VGPR lanes); VGPR spills must be 0
 BUDGETS = {
-    # the arena kernel (an experiment, AIRS_ARENA=1), DIFF and NONE, frames (5
-    # waves per SIMD); and its control-wave form (AIRS_ARENA_CTL)
-    "_ZN4airs12arena_kernelILi1ELb0ELb0ELb0EEEvNS_5KArgsE": (96, 17),
-    "_ZN4airs12arena_kernelILi0ELb0ELb0ELb0EEEvNS_5KArgsE": (96, 17),
-    "_ZN4airs12arena_kernelILi1ELb0ELb1ELb0EEEvNS_5KArgsE": (96, 28),
-    # the arena kernel with the fused per-frame Rice selection
-    "_ZN4airs12arena_kernelILi1ELb0ELb0ELb1EEEvNS_5KArgsE": (96, 0),
-    # cfg2 / cfg4: encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>
+    # cfg2 / cfg4: the Rice/ZERO frame kernel (enc_rice.hip), DIFF and NONE:
+    # five waves per SIMD at <= 96 VGPRs
+    "_ZN4airs11rice_kernelILi1ELb0EEEvNS_5KArgsE": (96, 8),
+    "_ZN4airs11rice_kernelILi0ELb0EEEvNS_5KArgsE": (96, 8),
+    # encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>: frames the Rice
+    # kernel does not take (k > 7, holes in device-planned launch lists)
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb0EEEvNS_5KArgsE": (128, 13),
     # cfg3: encode_kernel's fused per-frame Rice selection
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb1ELb0EEEvNS_5KArgsE": (128, 0),
-    # the frame walk with the per-frame Rice k (opt-in AIRS_FAUTO; 1024-thread workgroups: <= 128 VGPRs)
-    "_ZN4airs17frame_auto_kernelILi1EEEvNS_5KArgsE": (128, 18),
-    "_ZN4airs17frame_auto_kernelILi0EEEvNS_5KArgsE": (128, 11),
     # cfg2s: payload-only stream
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb1EEEvNS_5KArgsE": (128, 0),
     # cfg5 / cfg5fb: the context walk (1024-thread workgroups: <= 128 VGPRs)
@@ -63,7 +58,6 @@ def test_hot_kernel_register_budget(meta, sym):
 
 def test_every_kernel_is_gfx950_and_listed(meta):
     names = set(meta)
-    for stem in ("arena_kernel", "encode_kernel", "walk_ctx_kernel", "walk_kernel", "ck_chain_kernel",
-                 "select_rice_hist_kernel", "select_rice_pick_kernel", "fb_step_kernel", "dec_parse_kernel",
-                 "frame_auto_kernel"):
+    for stem in ("rice_kernel", "encode_kernel", "walk_ctx_kernel", "walk_kernel", "ck_chain_kernel",
+                 "select_rice_hist_kernel", "select_rice_pick_kernel", "fb_step_kernel", "dec_parse_kernel"):
         assert any(stem in n for n in names), stem
