@@ -140,7 +140,7 @@ struct airs_walk {
 	uint8_t *seq_out;         /* device [num_ctx], with fb */
 };
 int airs_dev_walk_supported(const struct airs_walk *w);
-uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_walk *w);
+uint32_t airs_dev_walk(struct airs_dev_engine *e, struct airs_walk *w);
 
 /* payload-only stream (cmp_gpu_encode_stream): the n samples at src (device)
  * as ONE bit stream from bit 0 of dst, no header or checksum; *status
@@ -209,7 +209,7 @@ uint32_t airs_dev_synth(struct airs_dev_engine *e, void *dst, uint32_t sample_by
 			uint32_t W);
 
 /* engine-owned scratch, grown on demand (stream ordered) */
-#define AIRS_NSLOT 15 /* scratch slots per engine; the last five are the device layer's (checksum
+#define AIRS_NSLOT 16 /* scratch slots per engine; the last five are the device layer's (checksum
 		       * placement, checksum products, decoder parse arrays, decoder frame info, IWT heads) */
 void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes);
 /* engine-owned page-locked host scratch, grown on demand: asynchronous
@@ -218,10 +218,27 @@ void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes);
 void *airs_dev_host_scratch(struct airs_dev_engine *e, size_t bytes);
 
 /* rewrite header bytes 8..13 (identifier) of launch frames whose status is
- * not an error: frame j = frame_add + j*frame_mul, identifier ids[j] (device) */
+ * not an error: frame j = frame_add + j*frame_mul, identifier ids[j] (device
+ * memory, or engine host scratch read over the bus) */
 uint32_t airs_dev_patch_ids(struct airs_dev_engine *e, void *dst, uint64_t dst_stride, uint32_t num_frames,
 			    uint32_t frame_add, uint32_t frame_mul, const uint64_t *ids,
 			    const uint32_t *status);
+
+/* The commit of a speculative batch, without a stream wait: begin launches
+ * one kernel that writes flags for the host (context c has a frame whose
+ * status is an error) and the fault count, signals, then waits for the host's
+ * release and patches identifiers if the release carries them (up to
+ * AIRS_HCO_MAX_IDS frames, ids[f] for frame f).  wait polls for the signal
+ * and copies the flags out (a fault count is returned as an error).
+ * release MUST follow every successful begin (with ids, or NULL: no patch),
+ * before any other wait on the stream; it returns 1 when the kernel patches
+ * the identifiers, 0 when the caller must (NULL, or more than the block
+ * holds). */
+#define AIRS_COMMIT_MAX_CTX 8192u /* contexts a commit kernel flags (AIRS_HCO_MAX_CTX) */
+uint32_t airs_dev_commit_begin(struct airs_dev_engine *e, const uint32_t *status, uint32_t num_ctx, uint32_t fpc,
+			       void *dst, uint64_t dst_stride, uint32_t *seq);
+uint32_t airs_dev_commit_wait(struct airs_dev_engine *e, uint32_t seq, uint32_t num_ctx, uint8_t *flags);
+int airs_dev_commit_release(struct airs_dev_engine *e, uint32_t seq, const uint64_t *ids, uint32_t total);
 
 /* decoder (decode.hip): frames at src + f*src_stride -> 16-bit samples at
  * dst + f*dst_stride bytes; status[f] = samples or error (see cmp_gpu.h) */
@@ -236,6 +253,9 @@ uint32_t airs_dev_h2d(struct airs_dev_engine *e, void *dst, const void *src, siz
 uint32_t airs_dev_d2h(struct airs_dev_engine *e, void *dst, const void *src, size_t bytes);
 uint32_t airs_dev_sync(struct airs_dev_engine *e);
 uint32_t airs_dev_memset(struct airs_dev_engine *e, void *dst, int v, size_t bytes);
+/* rows of `width` bytes, device to device: dst + r*dpitch <- src + r*spitch */
+uint32_t airs_dev_d2d_rows(struct airs_dev_engine *e, void *dst, size_t dpitch, const void *src, size_t spitch,
+			   size_t width, size_t rows);
 
 /* non-zero when a HIP device is usable */
 int airs_dev_available(void);

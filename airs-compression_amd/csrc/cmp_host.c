@@ -308,7 +308,7 @@ struct pass {
 	uint32_t hdr_bytes;
 };
 
-enum { SLOT_SRC = 0, SLOT_DST, SLOT_MODEL, SLOT_STATUS, SLOT_CK, SLOT_IDS, SLOT_G, SLOT_AUX, SLOT_FL, SLOT_SIZES };
+enum { SLOT_SRC = 0, SLOT_DST, SLOT_MODEL, SLOT_STATUS, SLOT_CK, SLOT_IDS, SLOT_G, SLOT_AUX, SLOT_FL, SLOT_SIZES, SLOT_MSAVE };
 
 /* The host-pointer API stages every frame through one process-wide engine
  * (device scratch slots, look-back state).  Calls on different contexts may
@@ -1620,6 +1620,8 @@ static uint32_t batch_walk_fb(struct cmp_gpu_engine *eng, struct cmp_context *ct
 		e = airs_dev_sync(dev);
 	if (is_err(e))
 		goto out;
+	/* the identifiers first; the contexts advance only once the headers are
+	 * patched (a failed upload or patch leaves them as they were) */
 	for (c = 0; c < num_ctx; c++) {
 		uint64_t id = ctx[c].identifier;
 
@@ -1629,12 +1631,7 @@ static uint32_t batch_walk_fb(struct cmp_gpu_engine *eng, struct cmp_context *ct
 			for (uint32_t k = 0; k < h_draws[f]; k++)
 				id = next_identifier();
 			ids[f] = id;
-			if (REPORT_DRAWS(b))
-				b->draws[f] = h_draws[f];
 		}
-		ctx[c].identifier = id;
-		ctx[c].sequence_number = h_seq[c];
-		ctx[c].model_size = 2u * n; /* every context's model holds a frame of this size */
 	}
 	{
 		/* upload from page-locked memory and patch, both asynchronous
@@ -1648,8 +1645,245 @@ static uint32_t batch_walk_fb(struct cmp_gpu_engine *eng, struct cmp_context *ct
 		else
 			e = airs_dev_patch_ids(dev, b->dst, b->dst_stride, total, 0, 1, d_ids, b->sizes);
 	}
+	if (is_err(e))
+		goto out;
+	for (c = 0; c < num_ctx; c++) {
+		for (a = 0; a < fpc; a++)
+			if (REPORT_DRAWS(b))
+				b->draws[c * fpc + a] = h_draws[c * fpc + a];
+		ctx[c].identifier = ids[c * fpc + fpc - 1u];
+		ctx[c].sequence_number = h_seq[c];
+		ctx[c].model_size = 2u * n; /* every context's model holds a frame of this size */
+	}
 out:
 	free(h_seq0);
+	return e;
+}
+
+/*
+ * MODEL contexts with the uncompressed fallback where the context walk does
+ * not apply (frames of another size, or too few contexts to fill the CUs):
+ * the segment walk codes every frame as if none fell back, with the raw frame
+ * size as the capacity, so a frame that would fall back reports DST_TOO_SMALL
+ * (the reference's first attempt, cmp.c:358-366) and nothing else changes for
+ * the frames that fit.  One read-back of the statuses; a context with such a
+ * frame (data that does not compress: rare) gets its model back from a copy
+ * taken before the launch and runs again on the per-acquisition device state
+ * machine (batch_device_exact), in call order, so the identifiers are drawn as
+ * the call loop draws them.  The other contexts' identifiers follow the pass
+ * rule (one draw per primary pass) and are patched into their headers.
+ * Returns 0, an error value, or WALK_NO.
+ */
+static uint32_t batch_walk_spec(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx, uint32_t fpc,
+				const struct cmp_gpu_batch *b, const struct pass *pp, const struct pass *ps, uint64_t *ids)
+{
+	struct airs_dev_engine *dev = eng->dev;
+	const struct cmp_params *P = &ctx[0].params;
+	const uint32_t bytes = b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
+	const uint32_t n = b->src_size / bytes, total = num_ctx * fpc;
+	const uint32_t raw = raw_frame_size(&ctx[0], n);
+	const size_t mb = 2u * (size_t)n; /* model bytes of a context */
+	struct airs_walk w;
+	uint32_t c, a, e = 0, seq_same = 1, m_strided = 1, msec = 0, cseq = 0, any_redo = 0;
+	uint64_t mbase, mstep;
+	uint8_t *msave, *redo = NULL, *hp;
+	uint32_t *new_seq = NULL;
+	uint64_t *new_id = NULL, *h_ids = NULL;
+
+	if (!model_needed(P) || !P->uncompressed_fallback_enabled || b->dst_capacity < raw || raw > 0xFFFFFFu ||
+	    (P->primary_preprocessing != CMP_PREPROCESS_NONE && P->primary_preprocessing != CMP_PREPROCESS_DIFF))
+		return WALK_NO;
+	if ((b->flags & CMP_GPU_AUTO_RICE) && P->primary_encoder_type == CMP_ENCODER_GOLOMB_ZERO)
+		return WALK_NO;
+	if (num_ctx > AIRS_COMMIT_MAX_CTX)
+		return WALK_NO;
+	for (c = 0; c < num_ctx; c++) {
+		const uint32_t sq = ctx[c].sequence_number;
+
+		if (!same_params(&ctx[c].params, P))
+			return WALK_NO;
+		if (sq != 0u && sq <= P->secondary_iterations && ctx[c].model_size != 2u * n)
+			return WALK_NO; /* the reference returns SRC_SIZE_MISMATCH for that frame */
+		if (sq != ctx[0].sequence_number)
+			seq_same = 0;
+	}
+	memset(&w, 0, sizeof(w));
+	w.src = b->src;
+	w.src_stride = b->src_stride;
+	w.sample_bytes = bytes;
+	w.is_unsigned = b->type == CMP_GPU_U16;
+	w.n = n;
+	w.num_ctx = num_ctx;
+	w.fpc = fpc;
+	w.dst = b->dst;
+	w.dst_stride = b->dst_stride;
+	w.cap = raw; /* the first attempt's capacity */
+	w.pre_p = P->primary_preprocessing;
+	w.enc_p = P->primary_encoder_type;
+	w.g_p = P->primary_encoder_param;
+	w.outl_p = P->primary_encoder_outlier;
+	w.enc_s = P->secondary_encoder_type;
+	w.g_s = P->secondary_encoder_param;
+	w.outl_s = P->secondary_encoder_outlier;
+	w.model_rate = P->model_rate;
+	w.iters = P->secondary_iterations;
+	w.checksum_enabled = P->checksum_enabled ? 1u : 0u;
+	w.status = b->sizes;
+	w.seq0 = ctx[0].sequence_number;
+	mbase = (uint64_t)(uintptr_t)ctx[0].work_buf;
+	mstep = num_ctx > 1 ? (uint64_t)(uintptr_t)ctx[1].work_buf - mbase : 0;
+	for (c = 0; c < num_ctx && m_strided; c++)
+		m_strided = (uint64_t)(uintptr_t)ctx[c].work_buf == mbase + c * mstep;
+	if (!m_strided)
+		for (c = 0; c < num_ctx; c++)
+			if ((uintptr_t)ctx[c].work_buf & 15u)
+				return WALK_NO;
+	w.model = (void *)(uintptr_t)mbase;
+	w.model_stride = m_strided ? mstep : 0;
+	/* identifiers 0: patched once they are drawn */
+	{
+		struct airs_walk chk = w;
+
+		if (!m_strided)
+			chk.model = NULL, chk.model_stride = 0;
+		if (!airs_dev_walk_supported(&chk))
+			return WALK_NO;
+	}
+	/* page-locked host scratch: the identifiers for patch_ids_kernel (when
+	 * the commit kernel does not take them) */
+	msave = airs_dev_scratch(dev, SLOT_MSAVE, mb * num_ctx);
+	hp = airs_dev_host_scratch(dev, (size_t)total * 8u);
+	new_seq = calloc(num_ctx, sizeof(*new_seq));
+	new_id = calloc(num_ctx, sizeof(*new_id));
+	redo = calloc(num_ctx, 1);
+	if (!msave || !hp || !new_seq || !new_id || !redo) {
+		e = ERRV(GENERIC);
+		goto out;
+	}
+	if (!m_strided) {
+		uint64_t *hp = malloc((size_t)num_ctx * 8u), *d_ptr = airs_dev_scratch(dev, SLOT_AUX, (size_t)num_ctx * 8u);
+
+		if (!hp || !d_ptr)
+			e = ERRV(GENERIC);
+		for (c = 0; c < num_ctx && !is_err(e); c++)
+			hp[c] = (uint64_t)(uintptr_t)ctx[c].work_buf;
+		if (!is_err(e))
+			e = airs_dev_h2d(dev, d_ptr, hp, (size_t)num_ctx * 8u);
+		if (!is_err(e))
+			e = airs_dev_sync(dev);
+		free(hp);
+		w.model_ptrs = d_ptr;
+	}
+	if (!seq_same && !is_err(e)) {
+		uint8_t *hs = malloc(num_ctx), *d_seq = airs_dev_scratch(dev, SLOT_FL, num_ctx);
+
+		if (!hs || !d_seq)
+			e = ERRV(GENERIC);
+		for (c = 0; c < num_ctx && !is_err(e); c++)
+			hs[c] = ctx[c].sequence_number;
+		if (!is_err(e))
+			e = airs_dev_h2d(dev, d_seq, hs, num_ctx);
+		if (!is_err(e))
+			e = airs_dev_sync(dev);
+		free(hs);
+		w.seq0s = d_seq;
+	}
+	/* the models as they are before the launch, for contexts run again whose
+	 * first frame reads its model (a secondary pass; a primary pass stores
+	 * the model without reading it) */
+	for (c = 0; c < num_ctx; c++)
+		if (ctx[c].sequence_number != 0u && ctx[c].sequence_number <= w.iters)
+			msec = 1;
+	if (!is_err(e) && msec) {
+		if (m_strided)
+			e = airs_dev_d2d_rows(dev, msave, mb, ctx[0].work_buf, num_ctx > 1 ? mstep : mb, mb, num_ctx);
+		else
+			for (c = 0; c < num_ctx && !is_err(e); c++)
+				e = airs_dev_d2d_rows(dev, msave + c * mb, mb, ctx[c].work_buf, mb, mb, 1);
+	}
+	if (!is_err(e) && P->checksum_enabled) {
+		uint32_t *d_ck = airs_dev_scratch(dev, SLOT_CK, (size_t)total * 4u);
+
+		e = d_ck ? airs_dev_checksum(dev, b->src, b->src_stride, bytes, n, total, NULL, d_ck) : ERRV(GENERIC);
+		w.checksums = d_ck;
+	}
+	/* the one round trip: which contexts have a frame that did not fit.  The
+	 * commit kernel signals them, then waits on the stream for the release
+	 * below (it patches the identifiers when no context runs again) */
+	h_ids = (uint64_t *)(void *)hp;
+	if (!is_err(e))
+		e = airs_dev_walk(dev, &w);
+	if (!is_err(e)) {
+		e = airs_dev_commit_begin(dev, b->sizes, num_ctx, fpc, b->dst, b->dst_stride, &cseq);
+		if (!is_err(e)) {
+			e = airs_dev_commit_wait(dev, cseq, num_ctx, redo);
+			for (c = 0; c < num_ctx && !is_err(e) && !any_redo; c++)
+				any_redo = redo[c];
+			if (is_err(e) || any_redo) {
+				(void)airs_dev_commit_release(dev, cseq, NULL, 0);
+				if (is_err(e)) {
+					(void)airs_dev_sync(dev); /* reports and clears the fault count */
+					goto out;
+				}
+			}
+		}
+	}
+	if (is_err(e))
+		goto out;
+	/* in call order: the pass rule's draws, or the context run again */
+	for (c = 0; c < num_ctx && !is_err(e); c++) {
+		if (!redo[c]) {
+			uint32_t sq = ctx[c].sequence_number;
+			uint64_t id = ctx[c].identifier;
+
+			for (a = 0; a < fpc; a++) {
+				const int prim = sq == 0u || sq > w.iters;
+
+				if (prim)
+					id = next_identifier();
+				ids[c * fpc + a] = id;
+				if (REPORT_DRAWS(b))
+					b->draws[c * fpc + a] = prim ? 1u : 0u;
+				sq = prim ? 1u : sq + 1u;
+			}
+			new_seq[c] = sq;
+			new_id[c] = id;
+		} else {
+			struct cmp_gpu_batch sb = *b;
+
+			if (msec)
+				e = airs_dev_d2d_rows(dev, ctx[c].work_buf, mb, msave + c * mb, mb, mb, 1);
+			sb.src = (const uint8_t *)b->src + (uint64_t)c * fpc * b->src_stride;
+			sb.dst = (uint8_t *)b->dst + (uint64_t)c * fpc * b->dst_stride;
+			sb.sizes = b->sizes + (size_t)c * fpc;
+			sb.draws = b->draws ? b->draws + (size_t)c * fpc : NULL;
+			if (!is_err(e))
+				e = batch_device_exact(eng, &ctx[c], 1, fpc, &sb, pp, ps, ids + (size_t)c * fpc);
+		}
+	}
+	if (is_err(e))
+		goto out;
+	/* the identifiers: released to the waiting commit kernel, or (a context
+	 * ran again, or more frames than its block holds) patched by
+	 * patch_ids_kernel from page-locked memory (batch_device_exact does not
+	 * use the host scratch) */
+	if (any_redo || !airs_dev_commit_release(dev, cseq, ids, total)) {
+		memcpy(h_ids, ids, (size_t)total * 8u);
+		e = airs_dev_patch_ids(dev, b->dst, b->dst_stride, total, 0, 1, h_ids, b->sizes);
+		if (is_err(e))
+			goto out;
+	}
+	for (c = 0; c < num_ctx; c++) {
+		if (redo[c])
+			continue; /* committed by batch_device_exact */
+		ctx[c].identifier = new_id[c];
+		ctx[c].sequence_number = (uint8_t)new_seq[c];
+		ctx[c].model_size = 2u * n;
+	}
+out:
+	free(new_seq);
+	free(new_id);
+	free(redo);
 	return e;
 }
 
@@ -1680,6 +1914,16 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 	if ((b->flags & CMP_GPU_REPORT_DRAWS) && !b->draws) {
 		fprintf(stderr, "airscmp: cmp_gpu_compress: CMP_GPU_REPORT_DRAWS without a draws array\n");
 		return ERRV(GENERIC);
+	}
+	if (b->draws && !(b->flags & CMP_GPU_REPORT_DRAWS)) {
+		/* callers of the earlier interface set draws alone: it is left
+		 * untouched now, say so once */
+		static int warned;
+		if (!warned) {
+			warned = 1;
+			fprintf(stderr, "airscmp: cmp_gpu_compress: draws array given without CMP_GPU_REPORT_DRAWS: "
+					"not written\n");
+		}
 	}
 	if (!b->dst)
 		return ERRV(DST_NULL);
@@ -1792,7 +2036,8 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 
 		memset(&ps, 0, sizeof(ps));
 		if (!(b->flags & (CMP_GPU_HOST_STEPPED | CMP_GPU_STEPWISE)) && device_exact_ok(ctx, num_ctx, b, n, &pp, &ps) &&
-		    (e = batch_walk_fb(eng, ctx, num_ctx, fpc, b, ids)) != WALK_NO)
+		    ((e = batch_walk_fb(eng, ctx, num_ctx, fpc, b, ids)) != WALK_NO ||
+		     (e = batch_walk_spec(eng, ctx, num_ctx, fpc, b, &pp, &ps, ids)) != WALK_NO))
 			; /* MODEL contexts with the fallback: every acquisition in one launch (or an error) */
 		else if (!(b->flags & CMP_GPU_HOST_STEPPED) && device_exact_ok(ctx, num_ctx, b, n, &pp, &ps))
 			e = batch_device_exact(eng, ctx, num_ctx, fpc, b, &pp, &ps, ids);

@@ -24,6 +24,17 @@
 #define AIRS_FAULT_WORD 16
 // engine->ticket[AIRS_WALK_TICKET]: the segment walk's logical block tickets
 #define AIRS_WALK_TICKET 32
+// the engine's coherent page-locked block (kernels write it over the bus,
+// the host polls it): words, per-context flags, identifiers
+#define AIRS_HCO_FAULT 0          // word: the fault count (airs_dev_sync, the commit kernel)
+#define AIRS_HCO_SEQ 1            // word: the commit kernel's signal (its sequence number)
+#define AIRS_HCO_GO 2             // word: the host's release of that kernel (the same number)
+#define AIRS_HCO_MODE 3           // word: 1 = patch the identifiers, 0 = not
+#define AIRS_HCO_FLAGS 64         // byte offset of the per-context flags
+#define AIRS_HCO_MAX_CTX 8192u    // flags for up to this many contexts
+#define AIRS_HCO_IDS (64u + 8192u) // byte offset of the identifiers
+#define AIRS_HCO_BYTES 65536u     // block size
+#define AIRS_HCO_MAX_IDS ((AIRS_HCO_BYTES - AIRS_HCO_IDS) / 8u)
 
 // Ablation switches (AIRS_DBG bits, benchmarking only) are compiled in only
 // with -DAIRS_ABLATE=1: in the product build every DBG() is a constant false,
@@ -505,6 +516,11 @@ uint32_t walk_ctx_samples();
 // samples per segment of the segment walk (walk_kernel): 4096 with four data
 // waves, 2048 with two (batches of few contexts); k.spf = n / that
 uint32_t walk_seg_samples(bool half);
+// the LDS bytes (dynamic + static) a walk launch takes, for the fit checks
+// against the CU's 160 KiB before a batch is routed to it
+size_t walk_ctx_lds(uint32_t img_words, uint32_t fpc);
+size_t walk_seg_lds(uint32_t img_words, uint32_t fpc);
+#define AIRS_LDS_BYTES (160u * 1024u)
 // the Rice/ZERO frame kernel (enc_rice.hip): 16-bit NONE/DIFF, one g = 2^k
 // (k <= 7), no model, whole 16 Ki-sample segments; false: not eligible
 bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s);

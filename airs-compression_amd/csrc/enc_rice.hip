@@ -16,9 +16,10 @@
 //     32-bit register: the two codewords back to back) and its length L
 //     (four lengths per register), instead of keeping the mapped values AND
 //     the code-table offsets: 40 registers per lane for the segment's 64
-//     samples instead of 64, so five workgroups (20 waves) fit a CU instead
-//     of four.  The table lookups move into phase 1, where they overlap the
-//     sample loads of the other workgroups; the packer reads no LDS at all;
+//     samples instead of 64.  The table lookups move into phase 1, where
+//     they overlap the sample loads of the other workgroups; the packer
+//     reads no LDS at all.  (Five workgroups per CU would fit the registers,
+//     but the look-back chains then stall: four);
 //   * the segment is packed back to back into ONE arena sized for a
 //     compressed segment (~15.7 bits per sample; a segment that does not
 //     fit is packed and stored chunk by chunk), so there is no image
@@ -138,6 +139,62 @@ __device__ __forceinline__ void pack_chunk(RPack &p, const uint32_t (&V)[8], con
 	}
 }
 
+// Evaluate a look-back from a first window (gv: granule gseg - 1 - lane,
+// newest first; tv: the predecessor's tail granule), reloading with vector
+// loads until the segment's frame bit offset is known: (offset, the
+// predecessor's last 32 bits).  Every published granule stays true, so the
+// first window may be of any age.
+__device__ __forceinline__ uint2 lb_resolve(const KArgs &a, uint32_t gseg, uint32_t sif, uint32_t lane, uint64_t gv,
+					    uint64_t tv, uint32_t rounds)
+{
+	const uint32_t first_seg = gseg - sif;
+	uint32_t sum = 0u, spins = 0u;
+	int64_t j = (int64_t)gseg - 1;
+	for (;;) {
+		const int64_t idx = j - (int64_t)lane;
+		const bool inr = idx >= (int64_t)first_seg;
+		const uint32_t tag = (uint32_t)(gv >> 32);
+		const bool valid = inr && (tag >> 1) == a.epoch;
+		const bool incl = valid && (tag & 1u);
+		const uint64_t incl_m = __ballot(incl);
+		const uint64_t bad_m = __ballot(inr && !valid);
+		const uint32_t fi = incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
+		const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
+		if (!(bad_m & need)) {
+			sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv : 0u);
+			if (incl_m)
+				break;
+			j -= 64; // every granule of this window is an aggregate: the next window
+			rounds++;
+		} else if (++spins > AIRS_SPIN_LIMIT) {
+			if (lane == 0)
+				atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u); // never expected (the host reports it)
+			break;
+		} else {
+			__builtin_amdgcn_s_sleep(1); // a needed predecessor has not published: re-poll
+			rounds++;
+		}
+		const int64_t nidx = j - (int64_t)lane;
+		gv = gran_load(&a.agg[nidx >= (int64_t)first_seg ? nidx : (int64_t)first_seg]);
+	}
+	// the predecessor's tail (lane 0's copy is the one used)
+	uint32_t s2 = 0;
+	for (; (uint32_t)(tv >> 32) != a.epoch; s2++) {
+		if (s2 > AIRS_SPIN_LIMIT) {
+			if (lane == 0)
+				atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+			break;
+		}
+		__builtin_amdgcn_s_sleep(1);
+		tv = gran_load(&a.tail[gseg - 1u]);
+	}
+	if (DBG(65536u) && a.dbgts && lane == 0) {
+		a.dbgts[8u * gseg + 5u] = ((uint64_t)spins << 32) | rounds;
+		a.dbgts[8u * gseg + 6u] = s2;
+	}
+	return make_uint2(sum, (uint32_t)tv);
+}
+
 // The look-back (wave 0): the segment's frame bit
 // offset P (header bits included) and the predecessor's last 32 bits.  The
 // first round reads the 16 newest granules and the tail through scalar loads
@@ -201,51 +258,7 @@ __device__ __forceinline__ uint2 rice_lookback(const KArgs &a, uint32_t gseg, ui
 		gv = gran_load(&a.agg[idx >= (int64_t)first_seg ? idx : (int64_t)first_seg]);
 		tv = gran_load(&a.tail[gseg - 1u]);
 	}
-	uint32_t sum = 0u, spins = 0u;
-	int64_t j = (int64_t)gseg - 1;
-	for (;;) {
-		const int64_t idx = j - (int64_t)lane;
-		const bool inr = idx >= (int64_t)first_seg;
-		const uint32_t tag = (uint32_t)(gv >> 32);
-		const bool valid = inr && (tag >> 1) == a.epoch;
-		const bool incl = valid && (tag & 1u);
-		const uint64_t incl_m = __ballot(incl);
-		const uint64_t bad_m = __ballot(inr && !valid);
-		const uint32_t fi = incl_m ? (uint32_t)__ffsll((unsigned long long)incl_m) - 1u : 64u;
-		const uint64_t need = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
-		if (!(bad_m & need)) {
-			sum += wave_sum((inr && lane <= fi) ? (uint32_t)gv : 0u);
-			if (incl_m)
-				break;
-			j -= 64; // every granule of this window is an aggregate: the next window
-			rounds++;
-		} else if (++spins > AIRS_SPIN_LIMIT) {
-			if (lane == 0)
-				atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u); // never expected (the host reports it)
-			break;
-		} else {
-			__builtin_amdgcn_s_sleep(1); // a needed predecessor has not published: re-poll
-			rounds++;
-		}
-		const int64_t nidx = j - (int64_t)lane;
-		gv = nidx >= (int64_t)first_seg ? gran_load(&a.agg[nidx]) : 0ull;
-	}
-	// the predecessor's tail (lane 0's copy is the one used)
-	uint32_t s2 = 0;
-	for (; (uint32_t)(tv >> 32) != a.epoch; s2++) {
-		if (s2 > AIRS_SPIN_LIMIT) {
-			if (lane == 0)
-				atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-			break;
-		}
-		__builtin_amdgcn_s_sleep(1);
-		tv = gran_load(&a.tail[gseg - 1u]);
-	}
-	if (DBG(65536u) && a.dbgts && lane == 0) {
-		a.dbgts[8u * gseg + 5u] = ((uint64_t)spins << 32) | rounds;
-		a.dbgts[8u * gseg + 6u] = s2;
-	}
-	return make_uint2(sum, (uint32_t)tv);
+	return lb_resolve(a, gseg, sif, lane, gv, tv, rounds);
 }
 
 // Store `tot` bits of an LDS image (bit 0 of word 0 = bit Pc of the frame)
@@ -320,16 +333,16 @@ __device__ __forceinline__ void rice_load(const KArgs &a, const uint8_t *fsrc, u
 			raw[c][0] = p[0];
 			raw[c][1] = p[1];
 		}
-		if (PRE == PRE_DIFF) {
-			const uint32_t pv = reinterpret_cast<const uint16_t *>(fsrc)[first ? first - 1u : 0u];
-			prevld[c] = first ? pv : 0u;
-		} else {
+		// (the caller zeroes it for the frame's first sample, at the use:
+		// a select here would make the compiler wait for the load)
+		if (PRE == PRE_DIFF)
+			prevld[c] = reinterpret_cast<const uint16_t *>(fsrc)[first ? first - 1u : 0u];
+		else
 			prevld[c] = 0u;
-		}
 	}
 }
 
-template <int PRE, bool PERSIST>
+template <int PRE>
 __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_WPE, 8))) void rice_kernel(KArgs a)
 {
 	constexpr uint32_t HDR_BITS = 176u; // 22-byte header (GOLOMB_ZERO)
@@ -343,17 +356,15 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 	const uint32_t nfr = a.num_segs / a.segs_per_frame;
 	// Frame-interleaved order (as encode_kernel): dispatch index d is segment
 	// d / nfr of launch frame d % nfr, so a frame's segments come in order.
-	// One segment per workgroup, d = the block index; PERSIST (experiment):
-	// workgroup b walks d = b, b + G, b + 2G, ... (G = the grid, all of it
-	// resident) with the next segment's samples loaded during this one's
-	// packing, look-back and stores.
-	uint32_t d = blockIdx.x;
-	uint32_t sif = d / nfr, lf = d - sif * nfr;
-	uint32_t gseg = lf * a.segs_per_frame + sif;
-	uint32_t frame = __builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
+	// One segment per workgroup, d = the block index.
+	const uint32_t d = blockIdx.x;
+	const uint32_t sif = d / nfr, lf = d - sif * nfr;
+	const uint32_t gseg = lf * a.segs_per_frame + sif;
+	const uint32_t frame =
+		__builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
 	if (frame == AIRS_NO_FRAME)
 		return;
-	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
+	const uint8_t *const fsrc = a.src + (uint64_t)frame * a.src_stride;
 	dbg_stamp(a, gseg, 0);
 
 	// ---- phase 0: every load of the segment, then zero the arena ----------
@@ -371,7 +382,6 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		s_tab[tid] = rice_table_entry(tid, k);
 	__syncthreads(); // B0: table and zeroed arena
 
-	for (;;) {
 	const bool is_first = sif == 0u, is_last = sif + 1u == a.segs_per_frame;
 	// ---- phase 1: codeword pairs and lengths -----------------------------
 	// V[c][j]: the codewords of samples 2j, 2j+1 of the lane's chunk c back to
@@ -386,8 +396,9 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		uint32_t m[8], q8[8];
 		// the pair ending with the sample before the lane's first: lane i - 1's
 		// last pair (DPP wave_shr:1), lane 0 the loaded sample
+		const uint32_t pv0 = (c == 0u && sif == 0u && wid == 0u) ? 0u : prevld[c]; // 0 before the frame's first sample
 		const uint32_t wprev = PRE == PRE_DIFF ? (uint32_t)__builtin_amdgcn_update_dpp(
-								 (int)(prevld[c] << 16), (int)w[7], 0x138, 0xF, 0xF, false)
+								 (int)(pv0 << 16), (int)w[7], 0x138, 0xF, 0xF, false)
 						       : 0u;
 #pragma unroll
 		for (uint32_t j = 0; j < 8u; j++) {
@@ -429,19 +440,6 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 #pragma unroll
 		for (uint32_t j = 0; j < 8u; j++)
 			asm volatile("" : "+v"(V[c][j]));
-	}
-
-	// PERSIST: the next segment's samples, in flight from here on
-	const uint32_t dn = d + gridDim.x;
-	uint32_t sif_n = 0u, lf_n = 0u, frame_n = 0u;
-	const uint8_t *fsrc_n = fsrc;
-	if (PERSIST) {
-		const uint32_t dl = dn < a.num_segs ? dn : d; // (past the end: this segment again, unused)
-		sif_n = dl / nfr;
-		lf_n = dl - sif_n * nfr;
-		frame_n = __builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf_n] : a.frame_add + lf_n * a.frame_mul);
-		fsrc_n = a.src + (uint64_t)frame_n * a.src_stride;
-		rice_load<PRE>(a, fsrc_n, sif_n, gseg, tid, raw, prevld);
 	}
 
 	// ---- block scan of the chunk totals (two chunks per register: a wave's
@@ -530,19 +528,6 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
 	}
 	dbg_stamp(a, gseg, 1);
-	// The look-back's window of 64 granules, read now and evaluated after the
-	// packing (wave 0, frames of >= 16 predecessors): the older granules of
-	// the window are mostly published by now, the 16 newest are read again
-	// by the scalar round at evaluation
-	uint64_t gearly = 0ull;
-#ifndef AIRS_RICE_EARLY
-#define AIRS_RICE_EARLY 0
-#endif
-	if (AIRS_RICE_EARLY && wid == 0 && sif >= AIRS_RICE_SLB) {
-		const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane, fs = (int64_t)(gseg - sif);
-		gearly = gran_load(&a.agg[idx >= fs ? idx : fs]);
-	}
-
 	uint8_t *fdst = a.dst + (uint64_t)frame * a.dst_stride;
 	const uint32_t cap = a.cap;
 	const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(fdst, 0, (int)(cap & ~3u), 0x00020000);
@@ -566,7 +551,7 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 				if (DBG(2u)) // ablation: no look-back (offsets invented, output garbage)
 					pp = make_uint2(HDR_BITS + sif * 37u, 0u);
 				else if (!is_first)
-					pp = rice_lookback(a, gseg, sif, lane, gearly);
+					pp = rice_lookback(a, gseg, sif, lane, 0ull);
 				if (lane == 0) {
 					if (!is_first)
 						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (pp.x + A));
@@ -671,24 +656,6 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		if (a.needed)
 			a.needed[frame] = size;
 	}
-	if (!PERSIST || dn >= a.num_segs)
-		break;
-	// every read of the arena is done: zero it for the next segment (its
-	// packing comes after the next B1)
-	__syncthreads();
-	{
-		uint4 *L4 = reinterpret_cast<uint4 *>(L_ar);
-		for (uint32_t i = tid; i < a.img_words / 4u; i += RWG)
-			L4[i] = make_uint4(0u, 0u, 0u, 0u);
-	}
-	d = dn;
-	sif = sif_n;
-	lf = lf_n;
-	gseg = lf * a.segs_per_frame + sif;
-	frame = frame_n;
-	fsrc = fsrc_n;
-	dbg_stamp(a, gseg, 0);
-	} // segments
 }
 
 // The launch, or false when it does not fit this kernel (the caller then
@@ -710,30 +677,10 @@ bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s)
 	ka.num_segs = nfr * ka.segs_per_frame;
 	ka.img_words = rice_arena_words();
 	const size_t lds = (size_t)ka.img_words * 4u;
-#ifndef AIRS_RICE_PERSIST
-#define AIRS_RICE_PERSIST 0
-#endif
-	if (AIRS_RICE_PERSIST && !k.frame_list) {
-		// experiment: the resident grid walks the segments (no hole lists)
-		static int per_cu = 0, cus = 0;
-		if (!cus) {
-			int dev = 0;
-			(void)hipGetDevice(&dev);
-			(void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-			(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rice_kernel<PRE_DIFF, true>, RWG, lds);
-		}
-		uint32_t grid = (uint32_t)(per_cu * cus);
-		grid = grid < ka.num_segs ? grid : ka.num_segs;
-		if (pre == PRE_DIFF)
-			hipLaunchKernelGGL((rice_kernel<PRE_DIFF, true>), dim3(grid), dim3(RWG), lds, s, ka);
-		else
-			hipLaunchKernelGGL((rice_kernel<PRE_NONE, true>), dim3(grid), dim3(RWG), lds, s, ka);
-		return true;
-	}
 	if (pre == PRE_DIFF)
-		hipLaunchKernelGGL((rice_kernel<PRE_DIFF, false>), dim3(ka.num_segs), dim3(RWG), lds, s, ka);
+		hipLaunchKernelGGL((rice_kernel<PRE_DIFF>), dim3(ka.num_segs), dim3(RWG), lds, s, ka);
 	else
-		hipLaunchKernelGGL((rice_kernel<PRE_NONE, false>), dim3(ka.num_segs), dim3(RWG), lds, s, ka);
+		hipLaunchKernelGGL((rice_kernel<PRE_NONE>), dim3(ka.num_segs), dim3(RWG), lds, s, ka);
 	return true;
 }
 

@@ -1403,6 +1403,32 @@ static bool walk_ctx_launch_p(const WArgs &k, uint32_t enc_p, bool rice_p, uint3
 	return false;
 }
 
+// walk_ctx_kernel's two images, then the deferred frame epilogues
+static size_t walk_ctx_lds_dyn(uint32_t img_words, uint32_t fpc)
+{
+	return (size_t)(2u * img_words + 4u) * 4u + (fpc <= AIRS_WALK_EPI_MAX ? (size_t)fpc * 16u : 0u);
+}
+
+// walk_kernel's images, then the deferred frame epilogues
+static size_t walk_seg_lds_dyn(uint32_t img_words, uint32_t fpc)
+{
+	return (size_t)(AIRS_WALK_NIMG * (img_words + 4u) + 4u) * 4u + (fpc <= AIRS_WALK_EPI_MAX ? (size_t)fpc * 16u : 0u);
+}
+
+// the static arrays of the two kernels (tables, wave sums, a few words),
+// bounded from above
+#define WALK_STATIC_LDS (2u * WTAB * 8u + 2u * 16u * 4u + 256u)
+
+size_t walk_ctx_lds(uint32_t img_words, uint32_t fpc)
+{
+	return walk_ctx_lds_dyn(img_words, fpc) + WALK_STATIC_LDS;
+}
+
+size_t walk_seg_lds(uint32_t img_words, uint32_t fpc)
+{
+	return walk_seg_lds_dyn(img_words, fpc) + WALK_STATIC_LDS;
+}
+
 uint32_t walk_ctx_samples()
 {
 	return 4u * CW_CHUNK;
@@ -1413,8 +1439,9 @@ bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint
 {
 	if (k.n != 4u * CW_CHUNK)
 		return false;
-	// walk_ctx_kernel's two images, then the deferred frame epilogues
-	const size_t lds = (size_t)(2u * k.img_words + 4u) * 4u + (k.fpc <= AIRS_WALK_EPI_MAX ? (size_t)k.fpc * 16u : 0u);
+	const size_t lds = walk_ctx_lds_dyn(k.img_words, k.fpc);
+	if (walk_ctx_lds(k.img_words, k.fpc) > AIRS_LDS_BYTES)
+		return false;
 	if (sample_bytes == 2)
 		return pre_p == PRE_DIFF ? walk_ctx_launch_p<2, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s)
 					 : walk_ctx_launch_p<2, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s);
@@ -1425,9 +1452,9 @@ bool walk_ctx_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint
 int walk_encode(const WArgs &k, uint32_t sample_bytes, uint32_t pre_p, uint32_t enc_p, bool rice_p, uint32_t enc_s,
 		bool rice_s, hipStream_t s, bool exclusive)
 {
-	// walk_kernel's images, then the deferred frame epilogues
-	const size_t lds = (size_t)(AIRS_WALK_NIMG * (k.img_words + 4u) + 4u) * 4u +
-			   (k.fpc <= AIRS_WALK_EPI_MAX ? (size_t)k.fpc * 16u : 0u);
+	const size_t lds = walk_seg_lds_dyn(k.img_words, k.fpc);
+	if (walk_seg_lds(k.img_words, k.fpc) > AIRS_LDS_BYTES)
+		return -1;
 	if (sample_bytes == 2)
 		return pre_p == PRE_DIFF ? walk_launch_p<2, PRE_DIFF>(k, enc_p, rice_p, enc_s, rice_s, lds, s, exclusive)
 					 : walk_launch_p<2, PRE_NONE>(k, enc_p, rice_p, enc_s, rice_s, lds, s, exclusive);

@@ -891,6 +891,58 @@ __global__ void patch_ids_kernel(uint8_t *dst, uint64_t stride, uint32_t num, ui
 		p[b] = (uint8_t)(id >> (40 - 8 * b));
 }
 
+// The speculative walk's commit (airs_dev_commit_*), one workgroup: flags[c]
+// = 1 when a frame of context c (frames c*fpc ..) has an error status, the
+// fault count, then (after a system-scope fence) the signal `seq`.  Then it
+// waits for the host's release (bounded: ~1 s of the 100 MHz clock) and, if
+// the release says so, writes the identifiers the host put in the block into
+// the headers of the frames without an error (as patch_ids_kernel).  The
+// stream's next work waits behind it, and no host launch is needed.
+__global__ void commit_kernel(const uint32_t *status, uint32_t num_ctx, uint32_t fpc, const uint32_t *ticket,
+			      volatile uint32_t *hco, uint32_t seq, uint8_t *dst, uint64_t dst_stride)
+{
+	__shared__ uint32_t s_mode;
+	volatile uint8_t *flags = reinterpret_cast<volatile uint8_t *>(hco) + AIRS_HCO_FLAGS;
+	for (uint32_t c = threadIdx.x; c < num_ctx; c += blockDim.x) {
+		uint32_t any = 0u;
+		for (uint32_t a = 0; a < fpc; a++)
+			any |= status[(uint64_t)c * fpc + a] > ERRV(128u) ? 1u : 0u;
+		flags[c] = (uint8_t)any;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		hco[AIRS_HCO_FAULT] = ticket[AIRS_FAULT_WORD];
+		__threadfence_system();
+		hco[AIRS_HCO_SEQ] = seq;
+		const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+		uint32_t mode = 0u;
+		for (;;) {
+			if (__hip_atomic_load(hco + AIRS_HCO_GO, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == seq) {
+				mode = hco[AIRS_HCO_MODE];
+				break;
+			}
+			if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull)
+				break; // no release: leave the headers alone
+			__builtin_amdgcn_s_sleep(8);
+		}
+		s_mode = mode;
+	}
+	__syncthreads();
+	if (s_mode != 1u)
+		return;
+	const volatile uint64_t *ids =
+		reinterpret_cast<const volatile uint64_t *>(reinterpret_cast<volatile uint8_t *>(hco) + AIRS_HCO_IDS);
+	const uint32_t total = num_ctx * fpc;
+	for (uint32_t f = threadIdx.x; f < total; f += blockDim.x) {
+		if (status[f] > ERRV(128u))
+			continue;
+		uint8_t *p = dst + (uint64_t)f * dst_stride + 8u;
+		const uint64_t id = ids[f];
+		for (int b = 0; b < 6; b++)
+			p[b] = (uint8_t)(id >> (40 - 8 * b));
+	}
+}
+
 // ---------------------------------------------------------------------
 // counter-hash synthetic frames (oracle orc_synth_u16 / orc_synth_i32)
 // ---------------------------------------------------------------------
@@ -981,6 +1033,8 @@ struct airs_dev_engine {
 	size_t rhist_cap; // frames
 	void *pinned; // page-locked host scratch (read-backs, identifier uploads)
 	size_t pinned_cap;
+	volatile uint32_t *hco; // coherent page-locked block (AIRS_HCO_*), written in-stream
+	uint32_t hco_seq;       // the last sequence word asked for
 	// cmp_gpu_engine_set_option (include/cmp_gpu.h)
 	uint32_t opt_exclusive;     // CMP_GPU_OPT_EXCLUSIVE
 	uint32_t opt_walk_segment;  // CMP_GPU_OPT_WALK_SEGMENT: 0, 2048 or 4096
@@ -1035,6 +1089,16 @@ extern "C" struct airs_dev_engine *airs_dev_engine_create(void *stream)
 		free(e);
 		return nullptr;
 	}
+	void *hf = nullptr;
+	if (hipHostMalloc(&hf, AIRS_HCO_BYTES, hipHostMallocCoherent) != hipSuccess) {
+		(void)hipFree(e->ticket);
+		free(e);
+		return nullptr;
+	}
+	e->hco = (volatile uint32_t *)hf;
+	e->hco[AIRS_HCO_FAULT] = 0u;
+	e->hco[AIRS_HCO_SEQ] = 0u;
+	e->hco[AIRS_HCO_GO] = 0u;
 	e->epoch = 0;
 	return e;
 }
@@ -1054,6 +1118,8 @@ extern "C" void airs_dev_engine_destroy(struct airs_dev_engine *e)
 		(void)hipFree(e->scratch[i]);
 	if (e->pinned)
 		(void)hipHostFree(e->pinned);
+	if (e->hco)
+		(void)hipHostFree((void *)e->hco);
 	free(e);
 }
 
@@ -1522,9 +1588,19 @@ static uint32_t ctx_walk_words(const struct airs_walk *w, bool no_ctx)
 	const uint32_t cw = ((walk_ctx_samples() / 4u * mb / 32u + 8u) + 3u) & ~3u;
 	if (no_ctx && !w->fb)
 		return 0u;
-	if (w->n == walk_ctx_samples() && w->num_ctx >= AIRS_WALK_CTX_MIN && (2u * cw + 4u) * 4u <= 150u * 1024u)
+	if (w->n == walk_ctx_samples() && w->num_ctx >= AIRS_WALK_CTX_MIN && (2u * cw + 4u) * 4u <= 150u * 1024u &&
+	    walk_ctx_lds(cw, w->fpc) <= AIRS_LDS_BYTES)
 		return cw;
 	return 0u;
+}
+
+// words of one image of the segment walk (walk_seg_samples(half) samples of
+// the longer-coded pass at its longest codeword, plus flush words)
+static uint32_t seg_walk_words(const struct airs_walk *w, bool half)
+{
+	const uint32_t mbp = code_max_bits(w->enc_p, w->g_p, w->outl_p);
+	const uint32_t mbs = code_max_bits(w->enc_s, w->g_s, w->outl_s);
+	return ((walk_seg_samples(half) * (mbp > mbs ? mbp : mbs) / 32u + 8u) + 3u) & ~3u;
 }
 
 extern "C" int airs_dev_walk_supported(const struct airs_walk *w)
@@ -1541,12 +1617,16 @@ extern "C" int airs_dev_walk_supported(const struct airs_walk *w)
 	if (w->fb && (!w->draws || !w->seq_out || w->cap != w->raw_size || w->raw_size < 16u + 2u * w->n ||
 		      !ctx_walk_words(w, false)))
 		return 0;
+	// the LDS of the launch the batch takes: the context walk, or the segment
+	// walk at its larger segment (either size may be chosen)
+	if (!ctx_walk_words(w, false) && walk_seg_lds(seg_walk_words(w, false), w->fpc) > AIRS_LDS_BYTES)
+		return 0;
 	const uint64_t segs = (uint64_t)w->num_ctx * (w->n / AIRS_SEG);
 	return segs <= 0x7FFFFFFFull && segs * w->fpc <= 0x7FFFFFFFull;
 }
 
 
-extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_walk *w)
+extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, struct airs_walk *w)
 {
 	if (!e || !airs_dev_walk_supported(w))
 		return ERRV(E_PARAMS_INVALID);
@@ -1600,16 +1680,14 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 	// one image for a segment of the longer-coded of the two passes at its
 	// longest codeword, plus flush words (cfg5's MULTI g = 8: 34 bits, 17 KiB;
 	// sized for 48 bits, two-data-wave workgroups did not all fit the CUs)
-	{
-		const uint32_t mbp = code_max_bits(w->enc_p, w->g_p, w->outl_p);
-		const uint32_t mbs = code_max_bits(w->enc_s, w->g_s, w->outl_s);
-		k.img_words = ((walk_seg_samples(half) * (mbp > mbs ? mbp : mbs) / 32u + 8u) + 3u) & ~3u;
-	}
+	k.img_words = seg_walk_words(w, half);
 	k.epoch = next_epoch(e);
 	// one context per workgroup when the frames have its size, there are
 	// enough contexts to fill the CUs, and two images fit the LDS
 	{
-		const uint32_t cw = ctx_walk_words(w, e->opt_no_ctx_walk != 0u);
+		// (CMP_GPU_OPT_NO_CONTEXT_WALK only where the segment walk fits)
+		const bool seg_fits = walk_seg_lds(seg_walk_words(w, false), w->fpc) <= AIRS_LDS_BYTES;
+		const uint32_t cw = ctx_walk_words(w, e->opt_no_ctx_walk != 0u && seg_fits);
 		if (cw) {
 			WArgs kc = k;
 			kc.img_words = cw;
@@ -1639,6 +1717,7 @@ extern "C" uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_w
 	k.ticket_base = e->walk_ticket_base;
 	const int wr = walk_encode(k, w->sample_bytes, w->pre_p, w->enc_p, true, w->enc_s, true, e->stream,
 				   e->opt_exclusive != 0u);
+
 	if (wr < 0)
 		return ERRV(E_PARAMS_INVALID);
 	HIPCHECK(hipGetLastError());
@@ -1869,6 +1948,18 @@ extern "C" uint32_t airs_dev_d2h(struct airs_dev_engine *e, void *dst, const voi
 	return 0;
 }
 
+extern "C" uint32_t airs_dev_d2d_rows(struct airs_dev_engine *e, void *dst, size_t dpitch, const void *src,
+				      size_t spitch, size_t width, size_t rows)
+{
+	if (!width || !rows)
+		return 0;
+	if (dpitch == width && spitch == width)
+		HIPCHECK(hipMemcpyAsync(dst, src, width * rows, hipMemcpyDeviceToDevice, e->stream));
+	else
+		HIPCHECK(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDeviceToDevice, e->stream));
+	return 0;
+}
+
 extern "C" uint32_t airs_dev_memset(struct airs_dev_engine *e, void *dst, int v, size_t bytes)
 {
 	if (!bytes)
@@ -1877,11 +1968,84 @@ extern "C" uint32_t airs_dev_memset(struct airs_dev_engine *e, void *dst, int v,
 	return 0;
 }
 
+// the fault count into the engine's coherent host word, in stream order
+__global__ void fault_copy_kernel(const uint32_t *ticket, volatile uint32_t *hco)
+{
+	hco[AIRS_HCO_FAULT] = ticket[AIRS_FAULT_WORD];
+}
+
+static uint32_t sync_wait(struct airs_dev_engine *e, bool waited);
+extern "C" int airs_dev_commit_release(struct airs_dev_engine *e, uint32_t seq, const uint64_t *ids, uint32_t total);
+
 extern "C" uint32_t airs_dev_sync(struct airs_dev_engine *e)
 {
-	uint32_t faults = 0;
-	HIPCHECK(hipStreamSynchronize(e->stream));
-	HIPCHECK(hipMemcpy(&faults, e->ticket + AIRS_FAULT_WORD, sizeof(faults), hipMemcpyDeviceToHost));
+	// one round trip: the fault word travels with the stream (a kernel writes
+	// it to coherent host memory) instead of a blocking copy after the wait
+	hipLaunchKernelGGL(fault_copy_kernel, dim3(1), dim3(1), 0, e->stream, e->ticket, e->hco);
+	HIPCHECK(hipGetLastError());
+	return sync_wait(e, false);
+}
+
+extern "C" uint32_t airs_dev_commit_begin(struct airs_dev_engine *e, const uint32_t *status, uint32_t num_ctx,
+					  uint32_t fpc, void *dst, uint64_t dst_stride, uint32_t *seq)
+{
+	if (num_ctx > AIRS_HCO_MAX_CTX)
+		return ERRV(E_PARAMS_INVALID);
+	*seq = ++e->hco_seq;
+	hipLaunchKernelGGL(commit_kernel, dim3(1), dim3(256), 0, e->stream, status, num_ctx, fpc, e->ticket, e->hco, *seq,
+			   (uint8_t *)dst, dst_stride);
+	HIPCHECK(hipGetLastError());
+	return 0;
+}
+
+// The host polls the kernel's signal in coherent memory instead of waiting
+// for the stream, whose wake-up is the larger part of a batch's round trip
+// (bounded; then the stream wait, which also reports a failed launch, after
+// the release so that the kernel is not left waiting)
+extern "C" uint32_t airs_dev_commit_wait(struct airs_dev_engine *e, uint32_t seq, uint32_t num_ctx, uint8_t *flags)
+{
+	for (uint64_t i = 0; i < (1ull << 26); i++) { // ~ a second of polls
+		if (e->hco[AIRS_HCO_SEQ] == seq) {
+			const uint32_t faults = e->hco[AIRS_HCO_FAULT];
+			memcpy(flags, (const void *)((const volatile uint8_t *)e->hco + AIRS_HCO_FLAGS), num_ctx);
+			if (faults) {
+				snprintf(g_err, sizeof(g_err), "%u look-back give-ups", faults);
+				fprintf(stderr, "airscmp: internal error: %s\n", g_err);
+				return ERRV(102u); /* CMP_ERR_INT_BITSTREAM: the caller releases, then airs_dev_sync clears */
+			}
+			return 0;
+		}
+		__builtin_ia32_pause();
+	}
+	(void)airs_dev_commit_release(e, seq, nullptr, 0u);
+	const uint32_t r = sync_wait(e, false);
+	if (r)
+		return r;
+	if (e->hco[AIRS_HCO_SEQ] != seq) {
+		snprintf(g_err, sizeof(g_err), "commit kernel did not signal");
+		return ERRV(E_GENERIC);
+	}
+	memcpy(flags, (const void *)((const volatile uint8_t *)e->hco + AIRS_HCO_FLAGS), num_ctx);
+	return 0;
+}
+
+extern "C" int airs_dev_commit_release(struct airs_dev_engine *e, uint32_t seq, const uint64_t *ids, uint32_t total)
+{
+	if (ids && total > AIRS_HCO_MAX_IDS)
+		ids = nullptr;
+	if (ids)
+		memcpy((void *)((volatile uint8_t *)e->hco + AIRS_HCO_IDS), ids, (size_t)total * 8u);
+	e->hco[AIRS_HCO_MODE] = ids ? 1u : 0u;
+	__atomic_thread_fence(__ATOMIC_SEQ_CST);
+	e->hco[AIRS_HCO_GO] = seq;
+	return ids ? 1 : 0;
+}
+
+static uint32_t sync_wait(struct airs_dev_engine *e, bool waited)
+{
+	if (!waited)
+		HIPCHECK(hipStreamSynchronize(e->stream));
+	const uint32_t faults = e->hco[AIRS_HCO_FAULT];
 #if AIRS_ABLATE
 	if ((g_dbg & 65536) && g_dbgts_path[0]) { // the debug timeline (scripts/ts_analyze.py)
 		FILE *f = fopen(g_dbgts_path, "wb");

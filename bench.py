@@ -99,6 +99,12 @@ WORKLOADS["cfg5s8"] = dict(WORKLOADS["cfg5"], nctx=32, shard=(0, 8),
 # those of cfg5: this data always compresses)
 WORKLOADS["cfg5fb"] = dict(WORKLOADS["cfg5"], desc=WORKLOADS["cfg5"]["desc"] + ", uncompressed fallback enabled",
                            params=dict(WORKLOADS["cfg5"]["params"], uncompressed_fallback_enabled=1))
+# rank 0's shard at N = 8 with the fallback enabled: 32 contexts are too few for
+# the context walk, so the batch takes the speculative segment walk (one launch,
+# then one read-back of the statuses; contexts with a frame that does not fit
+# run again on the device state machine: none here)
+WORKLOADS["cfg5fbs8"] = dict(WORKLOADS["cfg5s8"], desc=WORKLOADS["cfg5s8"]["desc"] + ", uncompressed fallback enabled",
+                             params=dict(WORKLOADS["cfg5"]["params"], uncompressed_fallback_enabled=1))
 
 
 def sample_bytes(wl):
@@ -334,6 +340,82 @@ class BufferSet:
         self.nbytes = self.src.numel() + self.dst.numel() + self.work.numel()
 
 
+def make_step(api, eng, wl, draws):
+    """One step: one cmp_gpu_compress call over a buffer set (or one payload-only
+    stream for cfg2s)."""
+    fpc = wl["fpc"]
+    flags = 1 if wl.get("auto_rice") else 0
+    nf = wl["nctx"] * fpc
+
+    def step(bs):
+        if wl.get("stream"):  # one payload-only stream over all the samples of the set
+            p = wl["params"]
+            r = eng.encode_stream(wl["kind"], bs.src.data_ptr(), nf * wl["n"], p["primary_preprocessing"],
+                                  p["primary_encoder_type"], p["primary_encoder_param"], 0, bs.dst.data_ptr(),
+                                  bs.dst.numel() - 64, bs.sizes.data_ptr())
+            if r:
+                raise RuntimeError("cmp_gpu_encode_stream: " + api.error_name(r))
+            return
+        r = eng.compress(bs.ctxs, fpc, wl["kind"], bs.src.data_ptr(), bs.stride, bs.stride, bs.dst.data_ptr(),
+                         bs.dstride, bs.cap, bs.sizes.data_ptr(), flags, draws.ctypes.data)
+        if r:
+            raise RuntimeError("cmp_gpu_compress: " + api.error_name(r))
+    return step
+
+
+def timed_steps(torch, stream, step, bsets, steps, warmup, sync):
+    """W untimed steps, then K timed ones bracketed by sync() and a device
+    synchronisation on both sides: (wall seconds, HIP-event ms per step)."""
+    for i in range(warmup):
+        step(bsets[i % len(bsets)])
+    torch.cuda.synchronize()
+    # one HIP event pair around the K steps (on the engine's stream): a
+    # pair per step would itself add ~8 us of stream time per step
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(steps):
+        step(bsets[i % len(bsets)])
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    sync()
+    wall = time.perf_counter() - t0
+    return wall, ev0.elapsed_time(ev1) / steps
+
+
+def make_sets(torch, pkg, lib, eng, wl, fids, rotate):
+    """The buffer sets the timed steps rotate over: enough that one rotation
+    touches more than the Infinity Cache (cold reads)."""
+    sets = [BufferSet(torch, pkg, lib, eng, wl, fids)]
+    rot = rotate or max(1, math.ceil(1.25 * INFINITY_CACHE / sets[0].nbytes))
+    rot = max(rot, 3) if sets[0].src.numel() < INFINITY_CACHE else rot
+    for _ in range(rot - 1):
+        sets.append(BufferSet(torch, pkg, lib, eng, wl, fids))
+    torch.cuda.synchronize()
+    return sets
+
+
+def scaling_reference_n1(torch, pkg, lib, eng, stream, steps, warmup):
+    """cfg4 on this one GPU (rank 0's 1024 frames at N = 1): the per-GPU work of
+    every N > 1 run, so that their value / (N x this) is the scaling
+    efficiency against the same workload (the N = 1 line itself is cfg2)."""
+    wl = WORKLOADS["cfg4"]
+    nf = wl["nctx"] * wl["fpc"]
+    draws = np.zeros(nf, dtype=np.uint8)
+    sets = make_sets(torch, pkg, lib, eng, wl, frame_ids(wl, 0, 1), 0)
+    wall, kern = timed_steps(torch, stream, make_step(pkg.cmpapi, eng, wl, draws), sets, steps, warmup, lambda: None)
+    del sets
+    torch.cuda.empty_cache()
+    return dict(workload="cfg4", n_gpus=1, frames=nf,
+                value=round(nf * 2 * wl["n"] * steps / wall / 1e9, 3), unit="GB/s",
+                ms_per_step=round(wall / steps * 1e3, 5), avg_step_gpu_ms=round(kern, 5),
+                note="the per-GPU workload of the N > 1 lines (cfg4: 1024 frames per GPU) on one GPU; "
+                     "weak-scaling efficiency at N = value_N / (N x this value)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -345,6 +427,8 @@ def main():
     ap.add_argument("--no-warm", action="store_true", help="skip the warm (one buffer set) replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--scaling-reference", action="store_true",
+                    help="with --workload at N = 1: also time cfg4 (the per-GPU work of the N > 1 runs)")
     args = ap.parse_args()
 
     import torch
@@ -392,50 +476,14 @@ def main():
     nf = nctx * fpc
     sb = sample_bytes(wl)
     fids = frame_ids(wl, rank, world)
-    flags = 1 if wl.get("auto_rice") else 0
 
-    sets = [BufferSet(torch, pkg, lib, eng, wl, fids)]
-    rot = args.rotate or max(1, math.ceil(1.25 * INFINITY_CACHE / sets[0].nbytes))
-    rot = max(rot, 3) if sets[0].src.numel() < INFINITY_CACHE else rot
-    for _ in range(rot - 1):
-        sets.append(BufferSet(torch, pkg, lib, eng, wl, fids))
-    torch.cuda.synchronize()
+    sets = make_sets(torch, pkg, lib, eng, wl, fids, args.rotate)
 
     draws = np.zeros(nf, dtype=np.uint8)  # identifier draws per frame (cmp_gpu_batch.draws), for the gather
+    step = make_step(api, eng, wl, draws)
 
-    def step(bs):
-        if wl.get("stream"):  # one payload-only stream over all the samples of the set
-            p = wl["params"]
-            r = eng.encode_stream(wl["kind"], bs.src.data_ptr(), nf * n, p["primary_preprocessing"],
-                                  p["primary_encoder_type"], p["primary_encoder_param"], 0, bs.dst.data_ptr(),
-                                  bs.dst.numel() - 64, bs.sizes.data_ptr())
-            if r:
-                raise RuntimeError("cmp_gpu_encode_stream: " + api.error_name(r))
-            return
-        r = eng.compress(bs.ctxs, fpc, wl["kind"], bs.src.data_ptr(), bs.stride, bs.stride, bs.dst.data_ptr(),
-                         bs.dstride, bs.cap, bs.sizes.data_ptr(), flags, draws.ctypes.data)
-        if r:
-            raise RuntimeError("cmp_gpu_compress: " + api.error_name(r))
-
-    def timed(bsets, steps, warmup):
-        for i in range(warmup):
-            step(bsets[i % len(bsets)])
-        torch.cuda.synchronize()
-        # one HIP event pair around the K steps (on the engine's stream): a
-        # pair per step would itself add ~8 us of stream time per step
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for i in range(steps):
-            step(bsets[i % len(bsets)])
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        barrier()
-        wall = time.perf_counter() - t0
-        return wall, ev0.elapsed_time(ev1) / steps
+    def timed(bsets, steps, warmup, sync=barrier):
+        return timed_steps(torch, stream, step, bsets, steps, warmup, sync)
 
     wall, kern_avg_ms = timed(sets, args.steps, args.warmup)
     t = torch.tensor([wall], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
@@ -448,6 +496,23 @@ def main():
         warm = dict(value=round(nf * sb * n * args.steps / wwall / 1e9, 3), ms_per_step=round(wwall / args.steps * 1e3, 5),
                     avg_step_gpu_ms=round(wkern, 5),
                     note="same K steps replayed on ONE buffer set (inputs may be served by the Infinity Cache)")
+
+    # ---- the single-GPU reference of the scaling runs (not in `value`) -----
+    scaling_ref = None
+    if world == 1 and wname != "cfg4" and (args.workload is None or args.scaling_reference):
+        scaling_ref = scaling_reference_n1(torch, pkg, lib, eng, stream, args.steps, args.warmup)
+    elif world > 1:
+        # rank 0 replays its own shard alone (the other ranks wait): the same
+        # per-GPU work with nothing else on the node
+        barrier()
+        if rank == 0:
+            swall, skern = timed(sets, args.steps, 2, sync=lambda: None)
+            scaling_ref = dict(workload=wname, n_gpus=1, frames=nf,
+                               value=round(nf * sb * n * args.steps / swall / 1e9, 3), unit="GB/s",
+                               ms_per_step=round(swall / args.steps * 1e3, 5), avg_step_gpu_ms=round(skern, 5),
+                               note="rank 0's shard replayed on its GPU alone after the timed run (other ranks "
+                                    "idle): the one-GPU rate of the per-GPU work")
+        barrier()
 
     # ---- bit-exactness against the reference's golden digests (every set) --
     gfile = "streams.json" if wl.get("stream") else "configs.json"
@@ -540,6 +605,10 @@ def main():
                   "per step, a 320-thread workgroup per (stream, %d-sample segment) walks the 16 acquisitions, each "
                   "acquisition's look-back resolved one step later" %
                   (8, 2048),
+        "cfg5fbs8": "airs::walk_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,8> (the segment walk of cfg5s8) with the raw "
+                    "frame size as capacity: ONE launch per step, then one read-back of the frame statuses and the "
+                    "identifier patch (patch_ids_kernel); a context with a frame that does not fit would run again on "
+                    "the device state machine (none in this data)",
         "cfg5fb": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> with the uncompressed fallback resolved on "
                   "the chip: ONE launch per step, then one read-back of the draw counts and the identifier patch "
                   "(patch_ids_kernel)",
@@ -605,6 +674,11 @@ def main():
         }
         if warm:
             result["warm"] = warm
+        if scaling_ref:
+            if world > 1:
+                scaling_ref["efficiency"] = round(value / (world * scaling_ref["value"]), 4)
+                scaling_ref["efficiency_note"] = "value / (n_gpus x the one-GPU rate of the same per-GPU work)"
+            result["scaling_reference"] = scaling_ref
         if gather:
             result["gather"] = gather
         print(json.dumps(result), flush=True)

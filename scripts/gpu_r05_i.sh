@@ -1,0 +1,13 @@
+# Round 5: product rice/walk/autorice parity, the pipelined experiment's parity, A/B cfg2/cfg4
+TAG=${1:-r05i}
+O=gpurun_out/$TAG
+cd "$GRAFT_REPO_ROOT" && mkdir -p $O && export TMPDIR=/tmp || exit 1
+timeout -k 10 120 python scripts/diag_pipe.py 2 0 laplace 40 2 exp/pipe/libairscmp.so > $O/diag.log 2>&1 && cat $O/diag.log || exit 1
+AIRS_LIB=exp/pipe/libairscmp.so timeout -k 10 600 python -u -m pytest tests/test_gpu_rice.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_p.log 2>&1
+rc=$?; tail -2 $O/pytest_p.log; [ $rc -eq 0 ] || exit $rc
+for rep in 1 2; do for w in cfg2 cfg4; do for lib in exp/old airs-compression_amd/lib exp/pipe; do
+  AIRS_LIB=$lib/libairscmp.so timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; print('$w $lib', d['ms_per_step'], d['bitexact_vs_reference'], r['avg_launch_ms_hip_events'], r['frac'])"
+done; done; done
+timeout -k 10 300 python bench.py --no-cpu-baseline --steps 20 --warmup 5 > $O/bench_def.json 2> $O/bench_def.err || { tail -5 $O/bench_def.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench_def.json')); print('default', d['ms_per_step'], d['bitexact_vs_reference'], d.get('scaling_reference'))"

@@ -157,7 +157,7 @@ int airs_dev_walk_supported(const struct airs_walk *w)
 
 unsigned long stub_walk_calls;
 
-uint32_t airs_dev_walk(struct airs_dev_engine *e, const struct airs_walk *w)
+uint32_t airs_dev_walk(struct airs_dev_engine *e, struct airs_walk *w)
 {
 	if (!e || !airs_dev_walk_supported(w) || !w->status)
 		return ERRV(10u);
@@ -404,9 +404,53 @@ uint32_t airs_dev_sync(struct airs_dev_engine *e)
 	return 0;
 }
 
+static uint8_t g_commit_flags[8192];
+
 uint32_t airs_dev_memset(struct airs_dev_engine *e, void *dst, int v, size_t bytes)
 {
 	(void)e;
 	memset(dst, v, bytes);
 	return 0;
+}
+
+uint32_t airs_dev_d2d_rows(struct airs_dev_engine *e, void *dst, size_t dpitch, const void *src, size_t spitch,
+			   size_t width, size_t rows)
+{
+	(void)e;
+	for (size_t r = 0; r < rows; r++)
+		memmove((uint8_t *)dst + r * dpitch, (const uint8_t *)src + r * spitch, width);
+	return 0;
+}
+
+uint32_t airs_dev_commit_begin(struct airs_dev_engine *e, const uint32_t *status, uint32_t num_ctx, uint32_t fpc,
+			       void *dst, uint64_t dst_stride, uint32_t *seq)
+{
+	(void)e;
+	(void)dst;
+	(void)dst_stride;
+	for (uint32_t c = 0; c < num_ctx && c < sizeof(g_commit_flags); c++) {
+		uint32_t any = 0;
+		for (uint32_t a = 0; a < fpc; a++)
+			any |= status[(size_t)c * fpc + a] > 0xFFFFFFFFu - 128u;
+		g_commit_flags[c] = (uint8_t)any;
+	}
+	*seq = 1;
+	return 0;
+}
+
+uint32_t airs_dev_commit_wait(struct airs_dev_engine *e, uint32_t seq, uint32_t num_ctx, uint8_t *flags)
+{
+	(void)e;
+	(void)seq;
+	memcpy(flags, g_commit_flags, num_ctx < sizeof(g_commit_flags) ? num_ctx : sizeof(g_commit_flags));
+	return 0;
+}
+
+int airs_dev_commit_release(struct airs_dev_engine *e, uint32_t seq, const uint64_t *ids, uint32_t total)
+{
+	(void)e;
+	(void)seq;
+	(void)ids;
+	(void)total;
+	return 0; /* the caller patches */
 }

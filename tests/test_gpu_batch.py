@@ -180,6 +180,51 @@ def test_batch_walk_fallback_cfg5_shape(prod, eng, orc, kind, flags):
     assert not bad, f"frames {bad[:8]} differ"
 
 
+@pytest.mark.parametrize("kind,n,nctx,p_noise", [("i16_in_i32", 65536, 32, 0.12), ("u16", 65536, 32, 0.0),
+                                                  ("u16", 16384, 8, 0.2), ("i16_in_i32", 8192, 3, 0.3)])
+def test_batch_segment_walk_fallback(prod, eng, orc, kind, n, nctx, p_noise):
+    """The fallback with too few contexts (or frames of another size) for the
+    context walk: the segment walk codes every frame with the raw frame size as
+    capacity; contexts with a frame that does not fit run again on the
+    per-acquisition device state machine from their models as they were before
+    the call (batch_walk_spec).  32 contexts of 64 Ki samples is rank 0's shard
+    of config 5 at N = 8 (cfg5fbs8); p_noise 0: no frame falls back (the
+    speculative walk's output stands).  Two calls on the same contexts.
+    Frames with identifiers unmasked, sizes, context states and work buffers
+    against the oracle's call loop."""
+    import numpy as np
+    P = api.CmpParams
+    params = P(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16,
+               secondary_iterations=15, secondary_preprocessing=3, secondary_encoder_type=2,
+               secondary_encoder_param=8, secondary_encoder_outlier=107, model_rate=11,
+               checksum_enabled=1, uncompressed_fallback_enabled=1)
+    rng = np.random.default_rng(n + nctx)
+    fpc = 5
+    srcs = []
+    for c in range(nctx):
+        base = np.cumsum(rng.integers(-3, 4, n))
+        for a in range(fpc):
+            if rng.random() < p_noise:
+                v = rng.integers(-32768, 32768, n)  # noise: the frame falls back
+            else:
+                v = base + rng.integers(-4, 5, n)
+            v = v.astype(np.int64)
+            if kind == "u16":
+                srcs.append((v & 0xFFFF).astype(np.uint16))
+            else:
+                srcs.append(((v & 0xFFFF) | (rng.integers(-5, 5, n) << 16)).astype(np.int32))
+    cap = 26 + 6 * n
+    splits = [2, 3]
+    want = bs.run_batch_host(orc, api, params, kind, n, nctx, fpc, cap, srcs, splits=splits)
+    heads = [api.parse_header(b) for r, b in want[0] if b is not None]
+    nfb = sum(1 for h in heads if h["encoder_type"] == 0)
+    assert (nfb > 0) == (p_noise > 0), nfb
+    got = bs.run_batch_gpu(prod, eng, api, params, kind, n, nctx, fpc, cap, srcs, splits=splits)
+    assert got[1] == want[1], "context states or work buffers differ"
+    bad = [f for f in range(nctx * fpc) if got[0][f] != want[0][f]]
+    assert not bad, f"frames {bad[:8]} differ"
+
+
 def test_batch_mixed_fallback_model_contexts(prod, eng, orc):
     """contexts with and without the uncompressed fallback
     in one batch (different parameters: the host-stepped path), with
