@@ -342,10 +342,12 @@ __device__ __forceinline__ void rice_load(const KArgs &a, const uint8_t *fsrc, u
 	}
 }
 
-template <int PRE>
+template <int PRE, bool STREAM>
 __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_WPE, 8))) void rice_kernel(KArgs a)
 {
-	constexpr uint32_t HDR_BITS = 176u; // 22-byte header (GOLOMB_ZERO)
+	// 22-byte header (GOLOMB_ZERO); STREAM (cmp_gpu_encode_stream): one frame,
+	// payload only (no header, checksum or 24-bit size field)
+	constexpr uint32_t HDR_BITS = STREAM ? 0u : 176u;
 	extern __shared__ __attribute__((aligned(16))) uint32_t L_ar[]; // RGUARD words, then the arena
 	__shared__ __attribute__((aligned(16))) uint2 s_tab[20];
 	__shared__ __attribute__((aligned(16))) uint32_t s_wsum[2][RNW];
@@ -537,7 +539,7 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 	const bool fits = (A >> 5) + 2u <= a.img_words - RGUARD;
 	// header bytes 20-21 (low half of the outlier field) share the frame's
 	// first payload word
-	const uint32_t hdr_pred = cd.outlier & 0xFFFFu;
+	const uint32_t hdr_pred = STREAM ? 0u : cd.outlier & 0xFFFFu;
 	__builtin_amdgcn_s_setprio(1);
 
 	if (fits) {
@@ -622,7 +624,13 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 
 	// ---- frame epilogue: checksum, header, status (the frame's last
 	// segment; as encode_kernel) ------------------------------------------
-	if (is_last && tid == 0) {
+	if (STREAM && is_last && tid == 0) {
+		const uint32_t payload_bytes = (s_misc[2] + A + 7u) >> 3;
+		a.status[frame] = payload_bytes > cap ? ERRV(E_DST_TOO_SMALL) : payload_bytes;
+		if (a.needed)
+			a.needed[frame] = payload_bytes;
+	}
+	if (!STREAM && is_last && tid == 0) {
 		const uint32_t P = s_misc[2];
 		const uint32_t n = a.n;
 		const uint32_t payload_bytes = (P + A + 7u) >> 3;
@@ -660,8 +668,10 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 
 // The launch, or false when it does not fit this kernel (the caller then
 // takes encode_kernel): 16-bit NONE/DIFF GOLOMB_ZERO with one g = 2^k,
-// k <= RICE_KMAX, for every frame, no model, whole segments of 16 Ki samples.
-bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s)
+// k <= RICE_KMAX, for every frame, no model, whole segments of 16 Ki samples
+// (stream: one payload-only frame, n <= AIRS_STREAM_MAX, so its bit offsets,
+// at most 24 bits per sample, stay below 2^32).
+bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s, bool stream)
 {
 	if (pre != PRE_NONE && pre != PRE_DIFF)
 		return false;
@@ -677,10 +687,12 @@ bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s)
 	ka.num_segs = nfr * ka.segs_per_frame;
 	ka.img_words = rice_arena_words();
 	const size_t lds = (size_t)ka.img_words * 4u;
-	if (pre == PRE_DIFF)
-		hipLaunchKernelGGL((rice_kernel<PRE_DIFF>), dim3(ka.num_segs), dim3(RWG), lds, s, ka);
+	void (*kern)(KArgs);
+	if (stream)
+		kern = pre == PRE_DIFF ? rice_kernel<PRE_DIFF, true> : rice_kernel<PRE_NONE, true>;
 	else
-		hipLaunchKernelGGL((rice_kernel<PRE_NONE>), dim3(ka.num_segs), dim3(RWG), lds, s, ka);
+		kern = pre == PRE_DIFF ? rice_kernel<PRE_DIFF, false> : rice_kernel<PRE_NONE, false>;
+	hipLaunchKernelGGL(kern, dim3(ka.num_segs), dim3(RWG), lds, s, ka);
 	return true;
 }
 

@@ -1265,7 +1265,7 @@ static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t 
 	// the Rice/ZERO frame kernel (enc_rice.hip)
 	if constexpr (AIRS_RICE && W == 2 && (PRE == PRE_NONE || PRE == PRE_DIFF) && ENC == ENC_ZERO && RICE &&
 		      MODEL == 0) {
-		if (full && rice_encode(k, PRE, s))
+		if (full && rice_encode(k, PRE, s, false))
 			return;
 	}
 	const size_t lds = (size_t)seg_images(W, MODEL) * (k.img_words + 4u) * 4u;
@@ -1763,6 +1763,12 @@ extern "C" uint32_t airs_dev_encode_stream(struct airs_dev_engine *e, const void
 	k.epoch = next_epoch(e);
 	const bool rice = encoder_param && (encoder_param & (encoder_param - 1u)) == 0u;
 	const bool full = n % segn == 0u && ((uintptr_t)src & 15u) == 0u;
+	// 16-bit GOLOMB_ZERO with g = 2^k, k <= 7: the Rice/ZERO kernel
+	if (AIRS_RICE && full && sample_bytes == 2 && encoder_type == ENC_ZERO && rice &&
+	    rice_encode(k, preprocessing, e->stream, true)) {
+		HIPCHECK(hipGetLastError());
+		return 0;
+	}
 	stream_encode(k, sample_bytes, preprocessing, encoder_type, rice, full, spf, e->stream);
 	HIPCHECK(hipGetLastError());
 	return 0;

@@ -594,8 +594,8 @@ def main():
             "arena per segment, decoupled look-back)")
     kernels = {
         "cfg2": rice + ": one launch per step",
-        "cfg2s": ("airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,-,STREAM> (enc_kernel.h: 16 Ki-sample segments): "
-                  "one launch per step, one look-back chain of 4096 segments"),
+        "cfg2s": ("airs::rice_kernel<DIFF,STREAM> (enc_rice.hip: 16 Ki-sample segments, no header): one launch "
+                  "per step, one look-back chain of 4096 segments"),
         "cfg3": ("airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO> (the per-frame Rice k chosen in-kernel from a "
                  "histogram of the samples in registers): one launch per step"),
         "cfg4": rice + ": one launch per step",

@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import rocpd_summary  # noqa: E402
 
 SAMPLES = {"cfg2": 64 << 20, "cfg2s": 64 << 20, "cfg3": 64 << 20, "cfg4": 64 << 20,
-           "cfg5": 256 << 20, "cfg5fb": 256 << 20, "cfg5s8": 32 << 20}
+           "cfg5": 256 << 20, "cfg5fb": 256 << 20, "cfg5s8": 32 << 20, "cfg5fbs8": 32 << 20}
 
 
 def main():
@@ -58,7 +58,7 @@ def main():
         # per-sample figures for the dominant encode kernel (most VALU; the
         # bench's input synthesis is not part of the path)
         enc = {k: v for k, v in out.get(wl, {}).items()
-               if "encode_kernel" in k or "walk_kernel" in k or "walk_ctx_kernel" in k}
+               if "encode_kernel" in k or "rice_kernel" in k or "walk_kernel" in k or "walk_ctx_kernel" in k}
         dom = max(enc.items(), key=lambda kv: kv[1].get("SQ_INSTS_VALU", 0), default=None)
         if dom:
             kn, r = dom

@@ -97,3 +97,34 @@ def test_stream_capacity_and_arguments(eng):
     assert api.error_name(gpu_stream(eng, x, c["kind"], 2, 1, 8, 0)[0]) == "PARAMS_INVALID"
     assert api.error_name(gpu_stream(eng, x, c["kind"], 3, 1, 8, 0)[0]) == "PARAMS_INVALID"
     assert api.error_name(gpu_stream(eng, x, c["kind"], 1, 1, 0, 0)[0]) == "PARAMS_INVALID"
+
+
+@pytest.mark.parametrize("k", range(0, 8))
+def test_stream_rice_kernel_vs_oracle(eng, k):
+    """Streams the Rice/ZERO frame kernel takes (16-bit,
+    GOLOMB_ZERO with g = 2^k, k <= 7, whole 16 Ki-sample segments, STREAM
+    mode: no header, the first payload bit at 0): laplace noise at the scale
+    of g, uniform noise (more bits than a segment's arena: chunk by chunk),
+    1, 7 and 65 segments (the scalar look-back round past 16), NONE and DIFF,
+    and a capacity one byte short."""
+    rng = np.random.default_rng(300 + k)
+    seg = 16384
+    bad = []
+    for m in (1, 7, 65):
+        for data in ("laplace", "uniform"):
+            n = m * seg
+            if data == "laplace":
+                v = np.round(rng.laplace(0, 2.0 ** k, n)).astype(np.int64)
+                v = np.cumsum(v) if m == 7 else v
+            else:
+                v = rng.integers(-32768, 32768, n)
+            kind = "u16" if (m + k) % 2 else "i16"
+            x = (v & 0xFFFF).astype(np.uint16) if kind == "u16" else (v & 0xFFFF).astype(np.uint16).view(np.int16)
+            for pre in (0, 1):
+                want = streams.oracle_stream(x, kind, pre, 1, 1 << k, 0)
+                got = gpu_stream(eng, x, kind, pre, 1, 1 << k, 0)
+                if got != want:
+                    bad.append((m, data, pre, got[0], want[0]))
+    assert not bad, bad
+    s, _ = gpu_stream(eng, x, kind, 1, 1, 1 << k, 0, cap=want[0] - 1)
+    assert api.error_name(s) == "DST_TOO_SMALL"

@@ -21,8 +21,8 @@ LIB = os.path.join(PKG_DIR, "lib", "libairscmp.so")
 BUDGETS = {
     # cfg2 / cfg4: the Rice/ZERO frame kernel (enc_rice.hip), DIFF and NONE:
     # five waves per SIMD at <= 96 VGPRs
-    "_ZN4airs11rice_kernelILi1EEEvNS_5KArgsE": (96, 8),
-    "_ZN4airs11rice_kernelILi0EEEvNS_5KArgsE": (96, 8),
+    "_ZN4airs11rice_kernelILi1ELb0EEEvNS_5KArgsE": (96, 8),
+    "_ZN4airs11rice_kernelILi0ELb0EEEvNS_5KArgsE": (96, 8),
     # encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>: frames the Rice
     # kernel does not take (k > 7, holes in device-planned launch lists)
     "_ZN4airs13encode_kernelILi2ELi1ELi1ELb1ELi0ELb1ELb0ELb0EEEvNS_5KArgsE": (128, 13),
