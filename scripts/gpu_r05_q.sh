@@ -1,4 +1,4 @@
-# Round 5: the Rice kernel with a control wave (look-back during the packing): parity, then A/B against HEAD
+# Round 5: Rice kernel A/B against the committed tree (exp/head): parity (rice + stream tests), cfg2 cfg4 cfg2s
 TAG=${1:-r05q}
 O=gpurun_out/$TAG
 cd "$GRAFT_REPO_ROOT" && mkdir -p $O && export TMPDIR=/tmp || exit 1

@@ -24,6 +24,8 @@ if os.environ.get("AIRS_KB_FRAMES"):  # scaling probe: more frames of the same s
     wl["fpc"] = int(os.environ["AIRS_KB_FRAMES"])
 stream = torch.cuda.current_stream()
 eng = lib.engine(stream.cuda_stream)
+if os.environ.get("AIRS_KB_EXCL"):  # the engine owns the device (CMP_GPU_OPT_EXCLUSIVE), as in bench.py
+    assert eng.set_option(pkg.OPT_EXCLUSIVE, 1) == 0
 n, nf = wl["n"], wl["nctx"] * wl["fpc"]
 stride = 2 * n
 # AIRS_KB_ROT=R: rotate over R input/output buffer sets (R >= 3 reads cold
