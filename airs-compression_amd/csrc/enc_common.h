@@ -66,11 +66,6 @@ struct KArgs {
 	const uint64_t *ids;
 	uint32_t *status;
 	uint32_t *needed;
-	// unused: keeps the later fields at the offsets for which the compiler
-	// allocates encode_kernel's scalar registers without spills (without it
-	// the cfg2 kernel spilled ~14 SGPRs to VGPR lanes, read back by ~140 more
-	// v_readlane, and ran 20 % slower: DESIGN.md 5.2)
-	const void *layout_pad;
 	uint64_t *agg;   // per segment: (epoch<<1 | inclusive) << 32 | bits
 	uint64_t *tail;  // per segment: epoch << 32 | last 32 bits of the segment's stream
 	uint32_t *ticket;
