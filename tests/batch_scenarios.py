@@ -93,7 +93,10 @@ def run_batch_host(lib, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=500
         lib.set_timestamp_func(None)
 
 
-def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000, flags=0, splits=None):
+def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start=5000, flags=0, splits=None,
+                  separate_work=False):
+    """separate_work: each context's work buffer its own allocation, at
+    uneven distances (the library then passes a pointer per context)."""
     import torch
     sb = 4 if kind == "i16_in_i32" else 2
     pcs = _per_ctx(params, nctx)
@@ -111,11 +114,16 @@ def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start
     try:
         wbs = max(_work_size(lib, api, p, stride) for p in pcs)
         wstride = (max(wbs, 2) + 15) // 16 * 16
-        work = torch.zeros(nctx * wstride, dtype=torch.uint8, device="cuda")
+        if separate_work:
+            works = [torch.zeros(wstride + 4096 * (c % 3), dtype=torch.uint8, device="cuda") for c in range(nctx)]
+            wptr = [t.data_ptr() for t in works]
+        else:
+            work = torch.zeros(nctx * wstride, dtype=torch.uint8, device="cuda")
+            wptr = [work.data_ptr() + c * wstride for c in range(nctx)]
         ctxs = (api.CmpContext * nctx)()
         for c in range(nctx):
             w = _work_size(lib, api, pcs[c], stride)
-            r = lib.initialise(ctxs[c], pcs[c], (work.data_ptr() + c * wstride) if w else None, w)
+            r = lib.initialise(ctxs[c], pcs[c], wptr[c] if w else None, w)
             assert not api.is_error(r), api.error_name(r)
         torch.cuda.synchronize()
         off = 0
@@ -127,13 +135,14 @@ def run_batch_gpu(lib, eng, api, params, kind, n, nctx, fpc, cap, srcs, ts_start
         assert eng.synchronize() == 0
         sz = sizes.cpu().numpy().astype(np.uint32)
         host = dst.cpu().numpy()
-        wk = work.cpu().numpy()
+        wk = [t.cpu().numpy()[:wbs] for t in works] if separate_work else \
+            [work.cpu().numpy()[c * wstride:c * wstride + wbs] for c in range(nctx)]
         frames = [None] * nf
         for j, f in enumerate(order):
             s = int(sz[j])
             frames[f] = (s, bytes(host[j * dstride:j * dstride + s]) if not api.is_error(s) else None)
-        state = [(ctxs[c].identifier, ctxs[c].sequence_number, ctxs[c].model_size,
-                  bytes(wk[c * wstride:c * wstride + wbs])) for c in range(nctx)]
+        state = [(ctxs[c].identifier, ctxs[c].sequence_number, ctxs[c].model_size, bytes(wk[c]))
+                 for c in range(nctx)]
         return tuple(frames), tuple(state)
     finally:
         lib.set_timestamp_func(None)

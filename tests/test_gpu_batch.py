@@ -180,16 +180,21 @@ def test_batch_walk_fallback_cfg5_shape(prod, eng, orc, kind, flags):
     assert not bad, f"frames {bad[:8]} differ"
 
 
-@pytest.mark.parametrize("kind,n,nctx,p_noise", [("i16_in_i32", 65536, 32, 0.12), ("u16", 65536, 32, 0.0),
-                                                  ("u16", 16384, 8, 0.2), ("i16_in_i32", 8192, 3, 0.3)])
-def test_batch_segment_walk_fallback(prod, eng, orc, kind, n, nctx, p_noise):
+@pytest.mark.parametrize("kind,n,nctx,p_noise,sep", [("i16_in_i32", 65536, 32, 0.12, False),
+                                                      ("u16", 65536, 32, 0.0, False),
+                                                      ("u16", 16384, 8, 0.2, False),
+                                                      ("i16_in_i32", 8192, 3, 0.3, False),
+                                                      ("u16", 16384, 6, 0.25, True)])
+def test_batch_segment_walk_fallback(prod, eng, orc, kind, n, nctx, p_noise, sep):
     """The fallback with too few contexts (or frames of another size) for the
     context walk: the segment walk codes every frame with the raw frame size as
     capacity; contexts with a frame that does not fit run again on the
     per-acquisition device state machine from their models as they were before
     the call (batch_walk_spec).  32 contexts of 64 Ki samples is rank 0's shard
     of config 5 at N = 8 (cfg5fbs8); p_noise 0: no frame falls back (the
-    speculative walk's output stands).  Two calls on the same contexts.
+    speculative walk's output stands); sep: work buffers in separate
+    allocations (a model pointer per context, saved and restored one by one).
+    Two calls on the same contexts.
     Frames with identifiers unmasked, sizes, context states and work buffers
     against the oracle's call loop."""
     import numpy as np
@@ -219,7 +224,7 @@ def test_batch_segment_walk_fallback(prod, eng, orc, kind, n, nctx, p_noise):
     heads = [api.parse_header(b) for r, b in want[0] if b is not None]
     nfb = sum(1 for h in heads if h["encoder_type"] == 0)
     assert (nfb > 0) == (p_noise > 0), nfb
-    got = bs.run_batch_gpu(prod, eng, api, params, kind, n, nctx, fpc, cap, srcs, splits=splits)
+    got = bs.run_batch_gpu(prod, eng, api, params, kind, n, nctx, fpc, cap, srcs, splits=splits, separate_work=sep)
     assert got[1] == want[1], "context states or work buffers differ"
     bad = [f for f in range(nctx * fpc) if got[0][f] != want[0][f]]
     assert not bad, f"frames {bad[:8]} differ"
