@@ -22,6 +22,8 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libairscmp.so")
 GPU_U16, GPU_I16, GPU_I16_IN_I32 = 0, 1, 2
 GPU_AUTO_RICE = 0x1
 REPORT_DRAWS = 0x8  # CMP_GPU_REPORT_DRAWS
+LAYOUT_ROUNDROBIN, LAYOUT_BLOCK, LAYOUT_STREAMS = 0, 1, 2  # enum cmp_gpu_layout
+GATHER_PATCH_IDS = 0x1  # CMP_GPU_GATHER_PATCH_IDS
 OPT_EXCLUSIVE = 1  # cmp_gpu_engine_set_option (include/cmp_gpu.h)
 OPT_WALK_SEGMENT = 2
 OPT_NO_CONTEXT_WALK = 3
@@ -117,9 +119,33 @@ class AirsLib(CmpLib):
         L.cmp_gpu_pack_frames.argtypes = [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_uint32, c_void_p,
                                           c_void_p]
         L.cmp_gpu_pack_frames.restype = c_uint32
+        L.cmp_gpu_gather.argtypes = [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_void_p, c_uint64, c_uint32,
+                                     c_void_p, c_void_p, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64,
+                                     c_uint32]
+        L.cmp_gpu_gather.restype = c_uint32
+        L.cmp_gpu_gather_plan.argtypes = [c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_uint64, c_void_p,
+                                          c_void_p, c_void_p, c_void_p]
+        L.cmp_gpu_gather_plan.restype = c_uint32
 
     def gpu_available(self) -> bool:
         return bool(self.lib.cmp_gpu_available())
+
+    def gather_plan(self, entries, world: int, frames_per_rank: int, layout: int, fpc: int = 1,
+                    id_base: int = 0, want_ids: bool = True):
+        """cmp_gpu_gather_plan on host arrays (no device): entries uint64
+        [world * frames_per_rank] = size | draws << 32.  Returns (rc,
+        rank_bytes, offsets, sizes, ids or None), the last three in global
+        frame order; ids UINT64_MAX where a frame keeps its identifier."""
+        import numpy as np
+        e = np.ascontiguousarray(entries, dtype=np.uint64)
+        n = world * frames_per_rank
+        rb = np.zeros(world, dtype=np.uint64)
+        offs = np.zeros(max(n, 1), dtype=np.uint64)
+        sz = np.zeros(max(n, 1), dtype=np.uint32)
+        ids = np.zeros(max(n, 1), dtype=np.uint64) if want_ids else None
+        r = self.lib.cmp_gpu_gather_plan(e.ctypes.data, world, frames_per_rank, layout, fpc, id_base, rb.ctypes.data,
+                                         offs.ctypes.data, sz.ctypes.data, ids.ctypes.data if want_ids else None)
+        return int(r), rb, offs[:n], sz[:n], (ids[:n] if want_ids else None)
 
     def engine(self, stream: int | None = None) -> "GpuEngine":
         return GpuEngine(self, stream)
@@ -187,6 +213,15 @@ class GpuEngine:
         """cmp_gpu_pack_frames: strided frames -> back to back at 8-byte aligned offsets (device)."""
         return self.lib.lib.cmp_gpu_pack_frames(self.handle, frames_ptr, frame_stride, frame_capacity, sizes_ptr,
                                                 num_frames, out_ptr, offsets_ptr)
+
+    def gather(self, nccl_comm: int, root: int, layout: int, fpc: int, frames_ptr: int, frame_stride: int,
+               frame_capacity: int, sizes_ptr: int, draws_ptr: int | None, frames_per_rank: int, out_ptr: int | None,
+               out_capacity: int, offsets_ptr: int | None, out_sizes_ptr: int | None, id_base: int = 0,
+               flags: int = 0) -> int:
+        """cmp_gpu_gather: every rank's frames on `root` over an RCCL communicator (ncclComm_t as an int)."""
+        return self.lib.lib.cmp_gpu_gather(self.handle, nccl_comm, root, layout, fpc, frames_ptr, frame_stride,
+                                           frame_capacity, sizes_ptr, draws_ptr, frames_per_rank, out_ptr,
+                                           out_capacity, offsets_ptr, out_sizes_ptr, id_base, flags)
 
     def synchronize(self) -> int:
         return self.lib.lib.cmp_gpu_synchronize(self.handle)

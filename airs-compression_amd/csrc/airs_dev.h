@@ -209,8 +209,9 @@ uint32_t airs_dev_synth(struct airs_dev_engine *e, void *dst, uint32_t sample_by
 			uint32_t W);
 
 /* engine-owned scratch, grown on demand (stream ordered) */
-#define AIRS_NSLOT 16 /* scratch slots per engine; the last five are the device layer's (checksum
+#define AIRS_NSLOT 19 /* scratch slots per engine; the last five are the device layer's (checksum
 		       * placement, checksum products, decoder parse arrays, decoder frame info, IWT heads) */
+#define AIRS_SLOT_GATHER 11 /* slots 11..13: cmp_gpu_gather (cmp_gather.c); 0..10 cmp_host.c */
 void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes);
 /* engine-owned page-locked host scratch, grown on demand: asynchronous
  * read-backs and uploads; the host may rewrite it once the stream has passed
@@ -239,6 +240,11 @@ uint32_t airs_dev_commit_begin(struct airs_dev_engine *e, const uint32_t *status
 			       void *dst, uint64_t dst_stride, uint32_t *seq);
 uint32_t airs_dev_commit_wait(struct airs_dev_engine *e, uint32_t seq, uint32_t num_ctx, uint8_t *flags);
 int airs_dev_commit_release(struct airs_dev_engine *e, uint32_t seq, const uint64_t *ids, uint32_t total);
+
+/* header bytes 8..13 of n frames at data + offsets[i] <- ids[i] (offsets and
+ * ids device arrays): the multi-GPU gather's identifier patch */
+uint32_t airs_dev_patch_ids_at(struct airs_dev_engine *e, void *data, const uint64_t *offsets, const uint64_t *ids,
+			       uint64_t n);
 
 /* decoder (decode.hip): frames at src + f*src_stride -> 16-bit samples at
  * dst + f*dst_stride bytes; status[f] = samples or error (see cmp_gpu.h) */

@@ -18,6 +18,7 @@
 #include "cmp_errors.h"
 #include "cmp_gpu.h"
 #include "airs_dev.h"
+#include "cmp_engine.h"
 
 #define ERRV(name) ((uint32_t)0u - (uint32_t)CMP_ERR_##name)
 #define CTX_MAGIC 34021395u      /* reference lib/compress/cmp.c:23 */
@@ -575,9 +576,6 @@ uint32_t cmp_compress_i16_in_i32(struct cmp_context *ctx, void *dst, uint32_t ds
 /* ================================================================== */
 /* device batch API (cmp_gpu.h)                                       */
 /* ================================================================== */
-struct cmp_gpu_engine {
-	struct airs_dev_engine *dev;
-};
 
 uint32_t cmp_gpu_decompress(struct cmp_gpu_engine *engine, const struct cmp_gpu_decode_batch *b)
 {

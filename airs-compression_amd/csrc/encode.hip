@@ -1924,6 +1924,28 @@ extern "C" uint32_t airs_dev_patch_ids(struct airs_dev_engine *e, void *dst, uin
 	return 0;
 }
 
+__global__ void patch_ids_at_kernel(uint8_t *data, const uint64_t *offsets, const uint64_t *ids, uint64_t n)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	uint8_t *p = data + offsets[i] + 8u;
+	const uint64_t id = ids[i];
+	for (int b = 0; b < 6; b++)
+		p[b] = (uint8_t)(id >> (40 - 8 * b));
+}
+
+extern "C" uint32_t airs_dev_patch_ids_at(struct airs_dev_engine *e, void *data, const uint64_t *offsets,
+					  const uint64_t *ids, uint64_t n)
+{
+	if (!e || !n)
+		return 0;
+	hipLaunchKernelGGL(patch_ids_at_kernel, dim3((uint32_t)((n + 255u) / 256u)), dim3(256), 0, e->stream,
+			   (uint8_t *)data, offsets, ids, n);
+	HIPCHECK(hipGetLastError());
+	return 0;
+}
+
 extern "C" void *airs_dev_malloc(size_t bytes)
 {
 	void *p = nullptr;

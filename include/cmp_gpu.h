@@ -180,6 +180,52 @@ uint32_t cmp_gpu_pack_frames(struct cmp_gpu_engine *engine, const void *frames, 
 			     uint32_t frame_capacity, const uint32_t *sizes, uint32_t num_frames, void *out,
 			     uint64_t *offsets);
 
+/*
+ * Multi-GPU gather of compressed frames, one call per rank
+ * of an RCCL communicator the caller owns (ncclComm_t, passed as void *; one
+ * process per GPU): every rank's frames (frame j of this rank at frames +
+ * j*frame_stride, sizes[j] bytes, as cmp_gpu_compress leaves them; sizes and
+ * frames device pointers) end up on `root`, packed at 8-byte aligned offsets
+ * in `out` (device, out_capacity bytes), with out_offsets / out_sizes (host,
+ * world * frames_per_rank entries) the frame table in GLOBAL frame order:
+ *   CMP_GPU_LAYOUT_ROUNDROBIN  rank r's frame j is global frame r + world*j
+ *   CMP_GPU_LAYOUT_BLOCK       rank r's frame j is global frame r*F + j
+ *   CMP_GPU_LAYOUT_STREAMS     streams of fpc frames, stream s on rank s mod world
+ * draws (host, per local frame; NULL: one each): cmp_gpu_batch.draws with
+ * CMP_GPU_REPORT_DRAWS.  With CMP_GPU_GATHER_PATCH_IDS the root rewrites each
+ * frame's header identifier (bytes 8..13) to what ONE process would have drawn
+ * for the node's frames in global order with the reference's default counter
+ * (cmp.c:27-50): id_base + the inclusive scan of the draws; a frame before its
+ * context's first draw keeps its identifier.  The frame layouts refuse the
+ * patch (CMP_ERR_PARAMS_INVALID on every rank) when a frame made no draw (a
+ * secondary pass depends on its rank's previous frame: use STREAMS).  Every
+ * rank decides from the same all-gathered table, so all ranks return the same
+ * refusal; a frame with an error value is refused the same way
+ * (CMP_ERR_GENERIC).  RCCL is loaded on first use.  The transfers are queued
+ * on the engine's stream; cmp_gpu_synchronize waits for them.  Build-defined
+ * extension (the C form of airs-compression_amd/shard.py).
+ */
+enum cmp_gpu_layout { CMP_GPU_LAYOUT_ROUNDROBIN = 0, CMP_GPU_LAYOUT_BLOCK = 1, CMP_GPU_LAYOUT_STREAMS = 2 };
+#define CMP_GPU_GATHER_PATCH_IDS 0x1u
+uint32_t cmp_gpu_gather(struct cmp_gpu_engine *engine, void *nccl_comm, uint32_t root, uint32_t layout, uint32_t fpc,
+			const void *frames, uint64_t frame_stride, uint32_t frame_capacity, const uint32_t *sizes,
+			const uint8_t *draws, uint32_t frames_per_rank, void *out, uint64_t out_capacity,
+			uint64_t *out_offsets, uint32_t *out_sizes, uint64_t id_base, uint32_t flags);
+
+/*
+ * The gather's plan on the host (no device, no RCCL): from the all-gathered
+ * table (entries[r * frames_per_rank + j] = size of rank r's frame j | its
+ * draws << 32), the packed bytes of each rank, and in global frame order each
+ * frame's offset in the root's buffer and size; ids (optional, world * F):
+ * the identifier to write, or UINT64_MAX for a frame that keeps its own.
+ * Returns 0, CMP_ERR_GENERIC (a frame carries an error value) or
+ * CMP_ERR_PARAMS_INVALID (layout / fpc, or a frame layout with a frame that
+ * made no draw while ids are requested).
+ */
+uint32_t cmp_gpu_gather_plan(const uint64_t *entries, uint32_t world, uint32_t frames_per_rank, uint32_t layout,
+			     uint32_t fpc, uint64_t id_base, uint64_t *rank_bytes, uint64_t *offsets, uint32_t *sizes,
+			     uint64_t *ids);
+
 /* wait for all work queued on the engine */
 uint32_t cmp_gpu_synchronize(struct cmp_gpu_engine *engine);
 
