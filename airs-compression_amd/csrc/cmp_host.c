@@ -1051,9 +1051,8 @@ out:
 }
 
 /*
- * Exact mode on the device.  When every context has the same parameters, no
- * pass is IWT (its transform is computed per launch into the work buffer)
- * and the prologue's static checks pass for both passes, the state machine
+ * Exact mode on the device.  When every context has the same parameters and
+ * the prologue's static checks pass for both passes, the state machine
  * that batch_exact() steps on the host runs on the GPU instead
  * (airs_dev_fb_step / airs_dev_fb_copy, airs_dev.h): per acquisition step a
  * planning kernel, the primary-pass launch, the secondary-pass launch (holes
@@ -1092,9 +1091,6 @@ static int device_exact_ok(const struct cmp_context *ctx, uint32_t num_ctx, cons
 	const struct cmp_params *P = &ctx[0].params;
 	uint32_t c, draws = 0;
 
-	if (P->primary_preprocessing == CMP_PREPROCESS_IWT ||
-	    (P->secondary_iterations && P->secondary_preprocessing == CMP_PREPROCESS_IWT))
-		return 0;
 	for (c = 0; c < num_ctx; c++) {
 		struct cmp_context t;
 		struct pass p;
@@ -1129,6 +1125,7 @@ static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_contex
 	const uint32_t bytes = b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
 	const uint32_t n = b->src_size / bytes, total = num_ctx * fpc;
 	const uint32_t cap1 = first_cap(&ctx[0], b, n), mneed = model_needed(P) ? 1u : 0u;
+	const uint32_t wneed = work_buf_state(P) ? 1u : 0u; /* the model, or IWT coefficients */
 	const size_t words = 4u * (size_t)num_ctx, tb = ((size_t)total + 15u) & ~(size_t)15u;
 	uint32_t *host_state = calloc(2u * (size_t)num_ctx, sizeof(uint32_t));
 	uint8_t *host_draws = calloc(total, 1);
@@ -1136,6 +1133,7 @@ static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_contex
 	uint32_t *d_ck = NULL, *d_g = NULL, c, a, e = 0;
 	uint64_t *d_ptr = NULL, mstride = 0;
 	void *mbase = NULL;
+	uint32_t mal16 = 0;
 	struct airs_fb_step S;
 
 	if (!host_state || !host_draws || !scr) {
@@ -1177,7 +1175,7 @@ static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_contex
 	if (!is_err(e))
 		e = airs_dev_memset(dev, S.fb, 0, tb);
 	/* work buffers: strided, or a pointer per context */
-	if (!is_err(e) && mneed) {
+	if (!is_err(e) && wneed) {
 		uint64_t base = (uint64_t)(uintptr_t)ctx[0].work_buf;
 		int ok = 1, al = 1;
 
@@ -1207,7 +1205,7 @@ static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_contex
 				S.model_ptrs = d_ptr;
 			}
 		}
-		(void)al;
+		mal16 = al;
 	}
 	if (!is_err(e) && P->checksum_enabled) {
 		d_ck = airs_dev_scratch(dev, SLOT_CK, (size_t)total * 4u);
@@ -1257,7 +1255,7 @@ static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_contex
 			L.model_stride = mstride;
 			L.model_div = fpc;
 			L.model_ptrs = d_ptr;
-			L.model_ptrs_al16 = 0;
+			L.model_ptrs_al16 = mal16;
 			/* a first attempt that runs out of room falls back, and the
 			 * fallback stores the whole model: no fail bit needed then */
 			L.fail_bit = S.fb_eligible ? UINT64_MAX : model_fail_bit(cap1, n);

@@ -179,6 +179,8 @@ __global__ __launch_bounds__(1024) void iwt_frame_kernel(IwtArgs a)
 	extern __shared__ int16_t L_iwt[];
 	uint32_t frame;
 	int16_t *coef = iwt_frame_coef(a, blockIdx.x, &frame);
+	if (frame == AIRS_NO_FRAME) // a hole of the launch's frame list (device exact mode)
+		return;
 	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
 	const uint32_t n = a.n, tid = threadIdx.x;
 	const IwtLds y{L_iwt};
@@ -239,6 +241,8 @@ __global__ __launch_bounds__(1024) void iwt_block_kernel(IwtArgs a)
 	__shared__ int16_t h_first[1024], h_odd[1024], heads[1024 + 64];
 	uint32_t frame;
 	int16_t *coef = iwt_frame_coef(a, blockIdx.x, &frame);
+	if (frame == AIRS_NO_FRAME) // a hole of the launch's frame list (device exact mode)
+		return;
 	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
 	const uint32_t n = a.n, nb = n / 64u, t = threadIdx.x;
 	const bool act = t < nb, last = t + 1u == nb;
@@ -320,6 +324,8 @@ __global__ __launch_bounds__(256) void iwt_blocks_a_kernel(IwtArgs a, uint32_t w
 	const uint32_t j = blockIdx.x / wg_per_frame, part = blockIdx.x - j * wg_per_frame;
 	uint32_t frame;
 	int16_t *coef = iwt_frame_coef(a, j, &frame);
+	if (frame == AIRS_NO_FRAME) // a hole of the launch's frame list (device exact mode)
+		return;
 	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
 	const uint32_t nb = a.n / 64u, t = threadIdx.x;
 	const int32_t gb = (int32_t)(part * IWT_RB + t) - 2; // global block of this thread
@@ -386,6 +392,8 @@ __global__ __launch_bounds__(64) void iwt_heads_b_kernel(IwtArgs a)
 	extern __shared__ int16_t L_heads[];
 	uint32_t frame;
 	int16_t *coef = iwt_frame_coef(a, blockIdx.x, &frame);
+	if (frame == AIRS_NO_FRAME) // a hole of the launch's frame list (device exact mode)
+		return;
 	const uint32_t nb = a.n / 64u, t = threadIdx.x;
 	const IwtLds y{L_heads};
 	const int16_t *hd = a.heads + (size_t)blockIdx.x * nb;
@@ -408,6 +416,8 @@ __global__ __launch_bounds__(256) void iwt_copy_kernel(IwtArgs a)
 {
 	uint32_t frame;
 	int16_t *coef = iwt_frame_coef(a, blockIdx.y, &frame);
+	if (frame == AIRS_NO_FRAME) // a hole of the launch's frame list (device exact mode)
+		return;
 	const uint8_t *fsrc = a.src + (uint64_t)frame * a.src_stride;
 	for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < a.n; i += gridDim.x * 256u)
 		coef[i] = iwt_sample<W>(fsrc, i);
@@ -417,6 +427,8 @@ __global__ __launch_bounds__(256) void iwt_level_kernel(IwtArgs a, uint32_t s, u
 {
 	uint32_t frame;
 	int16_t *coef = iwt_frame_coef(a, blockIdx.y, &frame);
+	if (frame == AIRS_NO_FRAME) // a hole of the launch's frame list (device exact mode)
+		return;
 	const uint32_t t0 = blockIdx.x * 256u + threadIdx.x, dt = gridDim.x * 256u;
 	if (evens)
 		iwt_evens(coef, a.n, s, t0, dt);
@@ -596,94 +608,192 @@ __global__ __launch_bounds__(64) void ck_chain_kernel(const uint8_t *src, uint64
 // ---------------------------------------------------------------------
 // Per-frame Rice parameter selection (build-defined rule; oracle
 // orc_select_rice_k): total_k = n(k+1) + sum_i min(v_i >> k, 16), v = m + 1.
-// A 128-bin histogram over (top-bit position t, next 3 bits) of v is a
-// sufficient statistic: for t - k >= 4 the term is 16, for 0 <= t - k <= 3 it
-// is the top (t-k+1) bits, for k > t it is 0.
+// The 129-bin histogram of enc_common.h (auto_term) is a sufficient statistic.
 // ---------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rice_key(uint32_t v) // v in [1, 65536]
-{
-	const uint32_t t = 31u - (uint32_t)__clz((int)v);
-	return t < 3u ? v : 8u + (t - 3u) * 8u + ((v >> (t - 3u)) & 7u);
-}
-
-__device__ __forceinline__ uint32_t key_term(uint32_t key, uint32_t k)
-{
-	if (key < 8u)
-		return min(key >> k, 16u);
-	const uint32_t t = (key - 8u) / 8u + 3u, top4 = 8u + ((key - 8u) & 7u);
-	if (k + 4u <= t)
-		return 16u;
-	if (k > t)
-		return 0u;
-	return top4 >> (k - (t - 3u)); // k in [t-3, t]
-}
-
 // Frames above AUTO_MAX_SPF segments (the fused path's limit), and MODEL
-// passes: the frame is split into slices of RICE_SLICE samples (a 4 Mi-sample
-// frame takes 128 workgroups).  Each slice builds its histogram in LDS and
-// adds the non-zero bins to the frame's global histogram (device atomics,
-// zeroed before the launch); select_rice_pick_kernel then takes the argmin of
-// the 16 totals, ties to the smaller k.
-#define RICE_SLICE (256u * AIRS_PT * 8u)
+// passes: a frame takes one workgroup per RICE_SLICE samples (a 4 Mi-sample
+// frame 64), which read its 4096-sample chunks interleaved.  Each workgroup
+// builds its histogram in LDS with
+// the fused path's layout (enc_kernel.h AUTO: the 129 bins of
+// enc_common.h auto_term, one 32-bit counter per bin and lane, so a wave's
+// atomics never share a bank) and adds the non-zero bins to the frame's
+// global histogram; the workgroup that arrives last (a per-frame counter) takes
+// the argmin of the 16 totals, ties to the smaller k, and writes g.
+#define RICE_SLICE (256u * AIRS_PT * 16u)
+#define RICE_HSTRIDE 132u // global words per launch frame: 129 bins, the arrival counter, pad
 template <int W, int PRE>
 __global__ __launch_bounds__(256) void select_rice_hist_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
 								const uint32_t *flist, uint32_t fadd, uint32_t fmul,
-								uint32_t *ghist)
+								uint32_t *ghist, uint32_t *out_g)
 {
-	__shared__ uint32_t hist[4][128];
-	const uint32_t tid = threadIdx.x, wid = tid >> 6;
+	__shared__ uint32_t H[AUTO_BINS * 64u];
+	__shared__ uint32_t s_bin[AUTO_BINS];
+	__shared__ uint32_t s_tot[16][17];
+	__shared__ uint32_t s_last;
+	const uint32_t tid = threadIdx.x, lane = tid & 63u;
 	const uint32_t frame = flist ? flist[blockIdx.x] : fadd + blockIdx.x * fmul;
 	if (frame == AIRS_NO_FRAME)
 		return;
 	const uint8_t *f = src + (uint64_t)frame * stride;
-	for (uint32_t i = tid; i < 4u * 128u; i += 256u)
-		(&hist[0][0])[i] = 0u;
+	for (uint32_t i = tid; i < sizeof(H) / 16u; i += 256u)
+		reinterpret_cast<uint4 *>(H)[i] = make_uint4(0u, 0u, 0u, 0u);
+	// lane's counter of bin b at byte hbase + 256 (b + 1016): b from the float bits
+	const uint32_t hbase = (uint32_t)(uintptr_t)H + 4u * lane - 1016u * 256u;
 	__syncthreads();
-	const uint32_t s0 = blockIdx.y * RICE_SLICE, s1 = min(n, s0 + RICE_SLICE);
-	for (uint32_t base = s0 + tid * AIRS_PT; base < s1; base += 256u * AIRS_PT) {
-		uint32_t x[AIRS_PT];
-		load16<W>(f, base, n, x);
-		uint32_t prev = 0u;
-		if (PRE == PRE_DIFF && base > 0u)
-			prev = sample_at<W>(f, base - 1u);
+	// one 16-sample group per lane and step, the next step's loads in flight
+	// while this one is binned (the step count is uniform: the shuffle below
+	// needs every lane of the wave).  Workgroup y takes the frame's 4096-sample
+	// chunks y, y + G, y + 2G, ... (G = gridDim.y): at any time the frame's
+	// workgroups read one contiguous span, not G spans a slice apart (which
+	// crowd a few HBM channels)
+	const uint32_t G = gridDim.y;
+	constexpr uint32_t CHN = 256u * AIRS_PT; // samples per chunk
+	const uint32_t chunks = (n + CHN - 1u) / CHN, y = blockIdx.y;
+	const uint32_t steps = chunks > y ? (chunks - y + G - 1u) / G : 0u;
+	const uint32_t step_n = G * CHN; // samples between this workgroup's chunks
+	auto bin1 = [&](uint32_t u, uint32_t inc) {
+		const int32_t d = (int32_t)(u << 16) >> 16;
+		const uint32_t v = (uint32_t)((d << 1) ^ (d >> 31)) + 1u;
+		const uint32_t ha = ((__float_as_uint((float)v) >> 20) << 8) + hbase;
+		__hip_atomic_fetch_add(reinterpret_cast<lds_u32 *>((uintptr_t)ha), inc, __ATOMIC_RELAXED,
+				       __HIP_MEMORY_SCOPE_WORKGROUP);
+	};
+	if (((uintptr_t)f & 15u) == 0u && n % CHN == 0u) {
+		// whole aligned chunks: straight-line loads of the raw words, every
+		// lane also loading the sample before its group (lane 0 uses it)
+		constexpr uint32_t RW = W; // uint4 per lane: 16 samples of W bytes
+		uint4 ra[RW], rb[RW];
+		uint32_t pa, pb;
+		auto ldraw = [&](uint4 (&r)[RW], uint32_t &p0, uint32_t b) {
+			const uint4 *q = reinterpret_cast<const uint4 *>(f + (size_t)b * W);
 #pragma unroll
-		for (int j = 0; j < AIRS_PT; j++) {
-			if (base + j < n) {
-				uint32_t u = PRE == PRE_DIFF ? x[j] - (j ? x[j - 1] : prev) : x[j];
-				u &= 0xFFFFu;
-				const uint32_t m = ((u << 1) ^ (0u - ((u >> 15) & 1u))) & 0xFFFFu;
-				atomicAdd(&hist[wid][rice_key(m + 1u)], 1u);
+			for (uint32_t i = 0; i < RW; i++)
+				r[i] = q[i];
+			p0 = PRE == PRE_DIFF ? sample_at<W>(f, b ? b - 1u : 0u) : 0u;
+		};
+		auto binraw = [&](const uint4 (&r)[RW], uint32_t p0, uint32_t inc) {
+			uint32_t x[AIRS_PT];
+#pragma unroll
+			for (uint32_t i = 0; i < RW; i++) {
+				const uint32_t w[4] = {r[i].x, r[i].y, r[i].z, r[i].w};
+#pragma unroll
+				for (uint32_t e = 0; e < 4u; e++) {
+					if (W == 2) {
+						x[8u * i + 2u * e] = w[e] & 0xFFFFu;
+						x[8u * i + 2u * e + 1u] = w[e] >> 16;
+					} else {
+						x[4u * i + e] = w[e] & 0xFFFFu;
+					}
+				}
 			}
+			uint32_t prev = 0u;
+			if (PRE == PRE_DIFF) {
+				// the sample before this lane's group: the previous lane's last one
+				prev = __shfl_up(x[AIRS_PT - 1], 1, 64);
+				if (lane == 0u)
+					prev = p0;
+			}
+#pragma unroll
+			for (int j = 0; j < AIRS_PT; j++)
+				bin1(PRE == PRE_DIFF ? x[j] - (j ? x[j - 1] : prev) : x[j], inc);
+		};
+		// two chunks per iteration, both loaded before either is binned, in
+		// one basic block so that the waits count exactly (a prefetch carried
+		// across iterations, or the second chunk binned under a branch, ended
+		// in over-waits); an odd last step bins its chunk twice, the second
+		// time adding 0
+		uint32_t base = y * CHN + tid * AIRS_PT;
+		for (uint32_t st = 0; st < steps; st += 2u, base += 2u * step_n) {
+			const bool two = st + 1u < steps;
+			ldraw(ra, pa, base);
+			ldraw(rb, pb, two ? base + step_n : base);
+			binraw(ra, pa, 1u);
+			binraw(rb, pb, two ? 1u : 0u);
+		}
+	} else {
+		// any other frame: 16 samples per lane and step, guarded
+		for (uint32_t st = 0, base = y * CHN + tid * AIRS_PT; st < steps; st++, base += step_n) {
+			uint32_t x[AIRS_PT];
+			load16<W>(f, base, n, x);
+			uint32_t prev = 0u;
+			if (PRE == PRE_DIFF) {
+				prev = __shfl_up(x[AIRS_PT - 1], 1, 64);
+				if (lane == 0u)
+					prev = base > 0u && base - 1u < n ? sample_at<W>(f, base - 1u) : 0u;
+			}
+#pragma unroll
+			for (int j = 0; j < AIRS_PT; j++)
+				if (base + j < n)
+					bin1(PRE == PRE_DIFF ? x[j] - (j ? x[j - 1] : prev) : x[j], 1u);
 		}
 	}
 	__syncthreads();
-	if (tid < 128u) {
-		const uint32_t c = hist[0][tid] + hist[1][tid] + hist[2][tid] + hist[3][tid];
-		if (c)
-			atomicAdd(&ghist[(uint64_t)blockIdx.x * 128u + tid], c);
-	}
-}
-
-__global__ __launch_bounds__(64) void select_rice_pick_kernel(uint32_t n, const uint32_t *flist, uint32_t fadd,
-							      uint32_t fmul, const uint32_t *ghist, uint32_t *out_g)
-{
-	__shared__ uint64_t tot[16];
-	const uint32_t tid = threadIdx.x;
-	const uint32_t frame = flist ? flist[blockIdx.x] : fadd + blockIdx.x * fmul;
-	if (frame == AIRS_NO_FRAME)
-		return;
-	const uint32_t *h = ghist + (uint64_t)blockIdx.x * 128u;
-	if (tid < 16u) {
-		uint64_t s = (uint64_t)n * (tid + 1u);
-		for (uint32_t key = 1; key < 128u; key++)
-			s += (uint64_t)h[key] * key_term(key, tid);
-		tot[tid] = s;
+	// bin totals: threads 2r, 2r+1 sum the halves of row r < 128; wave 0 row 128
+	{
+		const uint32_t r = tid >> 1, h = tid & 1u;
+		const uint4 *row = reinterpret_cast<const uint4 *>(H + r * 64u + h * 32u);
+		uint32_t t = 0u;
+#pragma unroll
+		for (uint32_t q = 0; q < 8u; q++) {
+			const uint4 v = row[(q + r) & 7u];
+			t += v.x + v.y + v.z + v.w;
+		}
+		t += __shfl_xor(t, 1, 64);
+		if (h == 0u)
+			s_bin[r] = t;
+		if (tid < 64u) {
+			uint32_t t128 = H[128u * 64u + lane];
+#pragma unroll
+			for (uint32_t o = 32u; o; o >>= 1)
+				t128 += __shfl_xor(t128, (int)o, 64);
+			if (lane == 0u)
+				s_bin[128] = t128;
+		}
 	}
 	__syncthreads();
-	if (tid == 0) {
-		uint32_t best = 0;
-		for (uint32_t k = 1; k < 16u; k++)
-			if (tot[k] < tot[best])
+	// The frame's histogram and arrival counter live in device memory and are
+	// touched by agent-scope atomics only, which execute at the memory side
+	// (MI355X_MICROARCH.md: atomics drop the line from the XCD's L2): no
+	// fence (__threadfence writes back and invalidates the caches, ~14 us per
+	// workgroup at four per CU).  Each bin add returns before the barrier, the
+	// arrival add after it; the last arrival reads the bins by exchanges, also
+	// at the memory side (an add of 0 may be turned into a cached load).
+	uint32_t *gh = ghist + (uint64_t)blockIdx.x * RICE_HSTRIDE;
+	if (tid < AUTO_BINS && s_bin[tid]) {
+		const uint32_t r = __hip_atomic_fetch_add(&gh[tid], s_bin[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		asm volatile("" ::"v"(r)); // a returning add: it has been performed once the value is back
+	}
+	__syncthreads();
+	if (tid == 0u)
+		s_last = __hip_atomic_fetch_add(&gh[AUTO_BINS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+			 gridDim.y - 1u;
+	__syncthreads();
+	if (!s_last)
+		return;
+	// the last slice: the frame's 16 candidate totals n(k+1) + sum_b h_b term(b, k)
+	if (tid < AUTO_BINS)
+		s_bin[tid] = __hip_atomic_exchange(&gh[tid], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	__syncthreads();
+	{
+		const uint32_t k = tid & 15u, sl = tid >> 4;
+		uint32_t part = 0u; // <= 16 n < 2^28
+		for (uint32_t b = sl; b < AUTO_BINS; b += 16u)
+			part += s_bin[b] * auto_term(b, k);
+		s_tot[k][sl] = part;
+	}
+	__syncthreads();
+	if (tid < 16u) {
+		uint32_t t = n * (tid + 1u);
+#pragma unroll
+		for (uint32_t sl = 0; sl < 16u; sl++)
+			t += s_tot[tid][sl];
+		s_tot[tid][16] = t;
+	}
+	__syncthreads();
+	if (tid == 0u) {
+		uint32_t best = 0u;
+		for (uint32_t k = 1u; k < 16u; k++)
+			if (s_tot[k][16] < s_tot[best][16])
 				best = k;
 		out_g[frame] = 1u << best;
 	}
@@ -1823,30 +1933,28 @@ extern "C" uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *
 		(void)hipFree(e->rhist);
 		e->rhist = nullptr;
 		e->rhist_cap = 0;
-		HIPCHECK(hipMalloc(&e->rhist, (size_t)num_frames * 128u * 4u));
+		HIPCHECK(hipMalloc(&e->rhist, (size_t)num_frames * RICE_HSTRIDE * 4u));
 		e->rhist_cap = num_frames;
 	}
-	HIPCHECK(hipMemsetAsync(e->rhist, 0, (size_t)num_frames * 128u * 4u, e->stream));
-	const dim3 grid(num_frames, (n + RICE_SLICE - 1u) / RICE_SLICE);
+	HIPCHECK(hipMemsetAsync(e->rhist, 0, (size_t)num_frames * RICE_HSTRIDE * 4u, e->stream));
+	const dim3 grid(num_frames, (n + RICE_SLICE - 1u) / RICE_SLICE); // <= 16 chunks per workgroup
 	if (grid.y > 65535u)
 		return ERRV(E_PARAMS_INVALID);
 	if (sample_bytes == 2) {
 		if (preprocessing == PRE_DIFF)
 			hipLaunchKernelGGL((select_rice_hist_kernel<2, PRE_DIFF>), grid, dim3(256), 0, e->stream, s, src_stride,
-					   n, flist, fadd, fmul, e->rhist);
+					   n, flist, fadd, fmul, e->rhist, out_g);
 		else
 			hipLaunchKernelGGL((select_rice_hist_kernel<2, PRE_NONE>), grid, dim3(256), 0, e->stream, s, src_stride,
-					   n, flist, fadd, fmul, e->rhist);
+					   n, flist, fadd, fmul, e->rhist, out_g);
 	} else {
 		if (preprocessing == PRE_DIFF)
 			hipLaunchKernelGGL((select_rice_hist_kernel<4, PRE_DIFF>), grid, dim3(256), 0, e->stream, s, src_stride,
-					   n, flist, fadd, fmul, e->rhist);
+					   n, flist, fadd, fmul, e->rhist, out_g);
 		else
 			hipLaunchKernelGGL((select_rice_hist_kernel<4, PRE_NONE>), grid, dim3(256), 0, e->stream, s, src_stride,
-					   n, flist, fadd, fmul, e->rhist);
+					   n, flist, fadd, fmul, e->rhist, out_g);
 	}
-	hipLaunchKernelGGL(select_rice_pick_kernel, dim3(num_frames), dim3(64), 0, e->stream, n, flist, fadd, fmul,
-			   (const uint32_t *)e->rhist, out_g);
 	HIPCHECK(hipGetLastError());
 	return 0;
 }

@@ -54,6 +54,37 @@ def test_batch_vs_call_loop(prod, eng, orc, exact_mode):
     assert errors > 50 and fallbacks > 50, (errors, fallbacks)
 
 
+@pytest.mark.parametrize("n,sec,spre", [(65536, 0, 1), (65536, 2, 2), (262144, 1, 2), (4160, 2, 3)])
+def test_batch_iwt_fallback_vs_call_loop(prod, eng, orc, exact_mode, n, sec, spre):
+    """IWT passes with the uncompressed fallback (round 5: the device exact
+    mode takes them; every IWT kernel form: the register kernel at 64 Ki,
+    the two-phase kernel above, the LDS frame kernel at 4160).  Smooth frames
+    compress, noise frames fall back, so the pass schedule of each context
+    changes mid-batch; frames, sizes and work buffers (the coefficients, or
+    the model) equal the call loop's."""
+    import numpy as np
+    P = api.CmpParams
+    rng = np.random.default_rng(n + sec)
+    params = P(primary_preprocessing=api.PREPROCESS_IWT, primary_encoder_type=1, primary_encoder_param=4,
+               secondary_iterations=sec, secondary_preprocessing=spre, secondary_encoder_type=1,
+               secondary_encoder_param=8, checksum_enabled=1, uncompressed_fallback_enabled=1, model_rate=5)
+    nctx, fpc = 3, 5
+    t = np.arange(n)
+    srcs = []
+    for f in range(nctx * fpc):
+        if rng.random() < 0.35:
+            srcs.append(rng.integers(0, 65536, n).astype(np.uint16))
+        else:
+            srcs.append((30000 + 8000 * np.sin(t / (50.0 + 7 * f)) + rng.integers(-20, 21, n)).astype(np.uint16))
+    cap = 16 + 2 * n + 4
+    want = bs.run_batch_host(orc, api, params, "u16", n, nctx, fpc, cap, srcs)
+    got = bs.run_batch_gpu(prod, eng, api, params, "u16", n, nctx, fpc, cap, srcs, flags=exact_mode)
+    assert got == want
+    frames = want[0]
+    raw = sum(1 for r, b in frames if b is not None and api.parse_header(b)["encoder_type"] == api.ENCODER_UNCOMPRESSED)
+    assert 0 < raw < len(frames), raw
+
+
 def test_batch_fallback_identifiers(prod, eng, orc, exact_mode):
     """Noise frames that do not compress: every frame falls back; identifiers
     advance by three draws per primary fallback and two per secondary one."""

@@ -62,5 +62,5 @@ def test_hot_kernel_register_budget(meta, sym):
 def test_every_kernel_is_gfx950_and_listed(meta):
     names = set(meta)
     for stem in ("rice_kernel", "encode_kernel", "walk_ctx_kernel", "walk_kernel", "ck_chain_kernel",
-                 "select_rice_hist_kernel", "select_rice_pick_kernel", "fb_step_kernel", "dec_parse_kernel"):
+                 "select_rice_hist_kernel", "fb_step_kernel", "dec_parse_kernel"):
         assert any(stem in n for n in names), stem
