@@ -729,11 +729,13 @@ static uint32_t raw_frame_size(const struct cmp_context *ctx, uint32_t n)
 }
 
 /* Launch cnt frames that share one pass: launch frame j is batch frame
- * fl[j] (host list) or add + j*mul; output capacity cap. */
+ * fl[j] (host list) or add + j*mul; output capacity cap.  coef (optional):
+ * the work buffer of launch frame j, in place of its context's (IWT frames
+ * of one context in one launch, batch_iwt). */
 static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t fpc,
 			     const struct cmp_gpu_batch *b, const struct frame_plan *plan, const uint32_t *fl,
 			     uint32_t add, uint32_t mul, uint32_t cnt, uint32_t cap, uint64_t *ids_scratch,
-			     uint64_t *ptr_scratch)
+			     uint64_t *ptr_scratch, const uint64_t *coef)
 {
 	struct airs_dev_engine *dev = eng->dev;
 	const uint32_t f0 = fl ? fl[0] : add;
@@ -785,9 +787,20 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 	}
 	if (P->model_mode != AIRS_MODEL_NONE || P->pre == CMP_PREPROCESS_IWT) {
 		for (j = 0; j < cnt; j++)
-			ptr_scratch[j] = (uint64_t)(uintptr_t)ctx[FRAME_AT(j) / fpc].work_buf;
+			ptr_scratch[j] = coef ? coef[j] : (uint64_t)(uintptr_t)ctx[FRAME_AT(j) / fpc].work_buf;
 		/* model of frame f = base + (f / fpc) * stride when the work buffers are strided */
-		{
+		if (coef) {
+			uint64_t *d_ptr = airs_dev_scratch(dev, SLOT_AUX, (size_t)cnt * 8u);
+
+			if (!d_ptr || is_err(airs_dev_h2d(dev, d_ptr, ptr_scratch, (size_t)cnt * 8u)) ||
+			    is_err(airs_dev_sync(dev)))
+				return ERRV(GENERIC);
+			L.model_ptrs = d_ptr;
+			L.model_ptrs_al16 = 1;
+			for (j = 0; j < cnt; j++)
+				if (ptr_scratch[j] & 15u)
+					L.model_ptrs_al16 = 0;
+		} else {
 			uint64_t base = (uint64_t)(uintptr_t)ctx[0].work_buf, mstep = 0;
 			uint32_t c, ok = 1, nctx = (nframes_total + fpc - 1) / fpc;
 
@@ -893,7 +906,7 @@ static uint32_t launch_groups(struct cmp_gpu_engine *eng, struct cmp_context *ct
 				done[k] = 1;
 			}
 		}
-		e = batch_launch(eng, ctx, fpc, b, plan, grp, 0, 1, g, caps[i], ids, ptrs);
+		e = batch_launch(eng, ctx, fpc, b, plan, grp, 0, 1, g, caps[i], ids, ptrs, NULL);
 	}
 	return e;
 }
@@ -1883,11 +1896,49 @@ out:
 	return e;
 }
 
+/*
+ * IWT contexts without a MODEL pass, every frame of the batch on the same
+ * pass (asynchronous mode): all frames in ONE launch instead of one per
+ * acquisition.  The reference computes a frame's coefficients into its
+ * context's work buffer (preprocess.c:321-353), so after the batch that
+ * buffer holds the coefficients of the context's last frame; the other
+ * frames' coefficients go to device scratch (at most IWT_SCRATCH_MAX bytes,
+ * else WALK_NO: the per-acquisition launches).
+ */
+#define IWT_SCRATCH_MAX (1ull << 30)
+static uint32_t batch_iwt(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx, uint32_t fpc,
+			  const struct cmp_gpu_batch *b, const struct frame_plan *plan, uint64_t *ids, uint64_t *ptrs)
+{
+	const uint32_t bytes = b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
+	const uint32_t n = b->src_size / bytes, total = num_ctx * fpc;
+	const uint64_t cstride = (2ull * n + 15u) & ~15ull;
+	const uint64_t need = (uint64_t)(total - num_ctx) * cstride;
+	uint64_t *coef, k = 0;
+	uint8_t *scr;
+	uint32_t c, a, e;
+
+	if (fpc < 2 || need > IWT_SCRATCH_MAX)
+		return WALK_NO;
+	scr = airs_dev_scratch(eng->dev, SLOT_MODEL, (size_t)need);
+	coef = malloc((size_t)total * sizeof(*coef));
+	if (!scr || !coef) {
+		free(coef);
+		return WALK_NO;
+	}
+	for (c = 0; c < num_ctx; c++)
+		for (a = 0; a < fpc; a++)
+			coef[c * fpc + a] = a + 1u == fpc ? (uint64_t)(uintptr_t)ctx[c].work_buf
+							  : (uint64_t)(uintptr_t)(scr + (k++) * cstride);
+	e = batch_launch(eng, ctx, fpc, b, plan, NULL, 0, 1, total, b->dst_capacity, ids, ptrs, coef);
+	free(coef);
+	return e == WALK_NO ? ERRV(GENERIC) : e;
+}
+
 uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, uint32_t num_ctx,
 			  uint32_t fpc, const struct cmp_gpu_batch *b)
 {
 	const uint32_t bytes = b && b->type == CMP_GPU_I16_IN_I32 ? 4u : 2u;
-	uint32_t n, c, a, total, e = 0, any_model = 0, exact = 0;
+	uint32_t n, c, a, total, e = 0, any_model = 0, any_mneed = 0, exact = 0;
 	struct frame_plan *plan;
 	uint64_t *ids, *ptrs;
 
@@ -1950,6 +2001,8 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		if (ctx[c].params.uncompressed_fallback_enabled &&
 		    b->dst_capacity >= raw_frame_size(&ctx[c], n))
 			exact = 1;
+		if (model_needed(&ctx[c].params))
+			any_mneed = 1;
 		if (work_buf_state(&ctx[c].params)) {
 			any_model = 1;
 			if ((uintptr_t)ctx[c].work_buf & 1u)
@@ -2053,7 +2106,7 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 
 			while (g < total && same_pass(&plan[g].p, &plan[f].p))
 				g++;
-			e = batch_launch(eng, ctx, fpc, b, plan, NULL, f, 1, g - f, b->dst_capacity, ids, ptrs);
+			e = batch_launch(eng, ctx, fpc, b, plan, NULL, f, 1, g - f, b->dst_capacity, ids, ptrs, NULL);
 			f = g;
 		}
 	} else {
@@ -2062,7 +2115,10 @@ uint32_t cmp_gpu_compress(struct cmp_gpu_engine *eng, struct cmp_context *ctx, u
 		for (f = 1; f < total && uniform; f++)
 			uniform = same_pass(&plan[f].p, &plan[0].p);
 		if (uniform && !any_model) {
-			e = batch_launch(eng, ctx, fpc, b, plan, NULL, 0, 1, total, b->dst_capacity, ids, ptrs);
+			e = batch_launch(eng, ctx, fpc, b, plan, NULL, 0, 1, total, b->dst_capacity, ids, ptrs, NULL);
+		} else if (uniform && !any_mneed && plan[0].p.pre == CMP_PREPROCESS_IWT && !(b->flags & CMP_GPU_STEPWISE) &&
+			   (e = batch_iwt(eng, ctx, num_ctx, fpc, b, plan, ids, ptrs)) != WALK_NO) {
+			/* IWT contexts: every frame in one launch (or an error) */
 		} else if (any_model && !(b->flags & CMP_GPU_STEPWISE) &&
 			   (e = batch_walk(eng, ctx, num_ctx, fpc, b, plan)) != WALK_NO) {
 			/* every acquisition in one launch (or an error) */

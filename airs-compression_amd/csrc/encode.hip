@@ -619,7 +619,10 @@ __global__ __launch_bounds__(64) void ck_chain_kernel(const uint8_t *src, uint64
 // atomics never share a bank) and adds the non-zero bins to the frame's
 // global histogram; the workgroup that arrives last (a per-frame counter) takes
 // the argmin of the 16 totals, ties to the smaller k, and writes g.
-#define RICE_SLICE (256u * AIRS_PT * 16u)
+#ifndef AIRS_RICE_SLICE_CH // 4096-sample chunks per workgroup
+#define AIRS_RICE_SLICE_CH 16u
+#endif
+#define RICE_SLICE (256u * AIRS_PT * AIRS_RICE_SLICE_CH)
 #define RICE_HSTRIDE 132u // global words per launch frame: 129 bins, the arrival counter, pad
 template <int W, int PRE>
 __global__ __launch_bounds__(256) void select_rice_hist_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
