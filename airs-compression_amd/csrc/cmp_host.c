@@ -842,7 +842,7 @@ static uint32_t batch_launch(struct cmp_gpu_engine *eng, struct cmp_context *ctx
 			return e;
 	}
 	if ((b->flags & CMP_GPU_AUTO_RICE) && P->enc == CMP_ENCODER_GOLOMB_ZERO &&
-	    (P->pre == CMP_PREPROCESS_NONE || P->pre == CMP_PREPROCESS_DIFF)) {
+	    (P->pre == CMP_PREPROCESS_NONE || P->pre == CMP_PREPROCESS_DIFF || P->pre == CMP_PREPROCESS_IWT)) {
 		d_g = airs_dev_scratch(dev, SLOT_G, (size_t)nframes_total * 4u);
 		if (!d_g)
 			return ERRV(GENERIC);
@@ -1258,7 +1258,7 @@ static uint32_t batch_device_exact(struct cmp_gpu_engine *eng, struct cmp_contex
 			L.encoder_param = Q->par;
 			L.outlier_param = Q->outlier_param;
 			if (d_g && Q->enc == CMP_ENCODER_GOLOMB_ZERO &&
-			    (Q->pre == CMP_PREPROCESS_NONE || Q->pre == CMP_PREPROCESS_DIFF)) {
+			    (Q->pre == CMP_PREPROCESS_NONE || Q->pre == CMP_PREPROCESS_DIFF || Q->pre == CMP_PREPROCESS_IWT)) {
 				L.auto_rice = 1;
 				L.frame_g_scratch = d_g;
 			}

@@ -625,9 +625,9 @@ __global__ __launch_bounds__(64) void ck_chain_kernel(const uint8_t *src, uint64
 #define RICE_SLICE (256u * AIRS_PT * AIRS_RICE_SLICE_CH)
 #define RICE_HSTRIDE 132u // global words per launch frame: 129 bins, the arrival counter, pad
 template <int W, int PRE>
-__global__ __launch_bounds__(256) void select_rice_hist_kernel(const uint8_t *src, uint64_t stride, uint32_t n,
-								const uint32_t *flist, uint32_t fadd, uint32_t fmul,
-								uint32_t *ghist, uint32_t *out_g)
+__global__ __launch_bounds__(256) void select_rice_hist_kernel(const uint8_t *src, uint64_t stride, uint32_t div,
+								const uint64_t *ptrs, uint32_t n, const uint32_t *flist,
+								uint32_t fadd, uint32_t fmul, uint32_t *ghist, uint32_t *out_g)
 {
 	__shared__ uint32_t H[AUTO_BINS * 64u];
 	__shared__ uint32_t s_bin[AUTO_BINS];
@@ -637,7 +637,9 @@ __global__ __launch_bounds__(256) void select_rice_hist_kernel(const uint8_t *sr
 	const uint32_t frame = flist ? flist[blockIdx.x] : fadd + blockIdx.x * fmul;
 	if (frame == AIRS_NO_FRAME)
 		return;
-	const uint8_t *f = src + (uint64_t)frame * stride;
+	// the frame's samples, or (IWT passes) its coefficients in the work buffer
+	// of the launch's model addressing: ptrs[j], or src + (frame / div) * stride
+	const uint8_t *f = ptrs ? reinterpret_cast<const uint8_t *>(ptrs[blockIdx.x]) : src + (uint64_t)(frame / div) * stride;
 	for (uint32_t i = tid; i < sizeof(H) / 16u; i += 256u)
 		reinterpret_cast<uint4 *>(H)[i] = make_uint4(0u, 0u, 0u, 0u);
 	// lane's counter of bin b at byte hbase + 256 (b + 1016): b from the float bits
@@ -1537,13 +1539,17 @@ static uint32_t run_iwt(struct airs_dev_engine *e, const struct airs_launch *L)
 	return 0;
 }
 
+static uint32_t select_rice(struct airs_dev_engine *e, const void *src, uint64_t src_stride, uint32_t div,
+			    const uint64_t *ptrs, uint32_t sample_bytes, uint32_t n, uint32_t num_frames,
+			    const uint32_t *flist, uint32_t fadd, uint32_t fmul, uint32_t preprocessing, uint32_t *out_g);
+
 extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs_launch *L)
 {
 	if (!e || !L || L->n == 0 || L->num_frames == 0)
 		return ERRV(E_GENERIC);
 	if (L->preprocessing > PRE_MODEL)
 		return ERRV(E_PARAMS_INVALID);
-	if (L->preprocessing == PRE_IWT && (L->frame_g || L->model_mode == AIRS_MODEL_UPDATE ||
+	if (L->preprocessing == PRE_IWT && (L->model_mode == AIRS_MODEL_UPDATE ||
 					    (!L->model && !L->model_ptrs)))
 		return ERRV(E_PARAMS_INVALID);
 	if (L->encoder_type > ENC_MULTI || (L->sample_bytes != 2 && L->sample_bytes != 4))
@@ -1562,11 +1568,25 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 				L->model_mode == AIRS_MODEL_NONE &&
 				(L->preprocessing == PRE_NONE || L->preprocessing == PRE_DIFF) && spf <= AUTO_MAX_SPF;
 	const uint32_t *frame_g = L->frame_g;
+	bool iwt_done = false;
 	if (L->auto_rice && !auto_fused && L->encoder_type == ENC_ZERO) {
-		if (!L->frame_g_scratch || (L->preprocessing != PRE_NONE && L->preprocessing != PRE_DIFF))
+		if (!L->frame_g_scratch || L->preprocessing == PRE_MODEL)
 			return ERRV(E_GENERIC);
-		r = airs_dev_select_rice(e, L->src, L->src_stride, L->sample_bytes, L->n, L->num_frames, L->frame_list,
-					 L->frame_add, L->frame_mul, L->preprocessing, L->frame_g_scratch);
+		if (L->preprocessing == PRE_IWT) {
+			// IWT passes: the coefficients first, then the selection over them
+			// (the IWT residual is the coefficient: NONE on 16-bit values)
+			r = run_iwt(e, L);
+			if (r)
+				return r;
+			iwt_done = true;
+			r = select_rice(e, L->model, L->model_stride, L->model_div ? L->model_div : 1u, L->model_ptrs, 2u, L->n,
+					L->num_frames, L->frame_list, L->frame_add, L->frame_list ? 0u : L->frame_mul, PRE_NONE,
+					L->frame_g_scratch);
+		} else {
+			r = select_rice(e, L->src, L->src_stride, 1u, nullptr, L->sample_bytes, L->n, L->num_frames,
+					L->frame_list, L->frame_add, L->frame_list ? 0u : L->frame_mul, L->preprocessing,
+					L->frame_g_scratch);
+		}
 		if (r)
 			return r;
 		frame_g = L->frame_g_scratch;
@@ -1644,7 +1664,7 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 		    (L->encoder_param && (L->encoder_param & (L->encoder_param - 1u)) == 0u);
 	if (L->preprocessing == PRE_MODEL && L->model_mode != AIRS_MODEL_UPDATE)
 		return ERRV(E_PARAMS_INVALID);
-	if (L->preprocessing == PRE_IWT) {
+	if (L->preprocessing == PRE_IWT && !iwt_done) {
 		r = run_iwt(e, L);
 		if (r)
 			return r;
@@ -1923,12 +1943,12 @@ extern "C" uint32_t airs_dev_checksum(struct airs_dev_engine *e, const void *src
 	return 0;
 }
 
-extern "C" uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
-					 uint32_t sample_bytes, uint32_t n, uint32_t num_frames,
-					 const uint32_t *flist, uint32_t fadd, uint32_t fmul, uint32_t preprocessing,
-					 uint32_t *out_g)
+// the sliced selection over frame f at src + (f / div) * stride, or ptrs[j]
+static uint32_t select_rice(struct airs_dev_engine *e, const void *src, uint64_t src_stride, uint32_t div,
+			    const uint64_t *ptrs, uint32_t sample_bytes, uint32_t n, uint32_t num_frames,
+			    const uint32_t *flist, uint32_t fadd, uint32_t fmul, uint32_t preprocessing, uint32_t *out_g)
 {
-	if (!e || !n || !num_frames)
+	if (!e || !n || !num_frames || !div)
 		return ERRV(E_GENERIC);
 	const uint8_t *s = (const uint8_t *)src;
 	if (num_frames > e->rhist_cap) {
@@ -1946,20 +1966,29 @@ extern "C" uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *
 	if (sample_bytes == 2) {
 		if (preprocessing == PRE_DIFF)
 			hipLaunchKernelGGL((select_rice_hist_kernel<2, PRE_DIFF>), grid, dim3(256), 0, e->stream, s, src_stride,
-					   n, flist, fadd, fmul, e->rhist, out_g);
+					   div, ptrs, n, flist, fadd, fmul, e->rhist, out_g);
 		else
 			hipLaunchKernelGGL((select_rice_hist_kernel<2, PRE_NONE>), grid, dim3(256), 0, e->stream, s, src_stride,
-					   n, flist, fadd, fmul, e->rhist, out_g);
+					   div, ptrs, n, flist, fadd, fmul, e->rhist, out_g);
 	} else {
 		if (preprocessing == PRE_DIFF)
 			hipLaunchKernelGGL((select_rice_hist_kernel<4, PRE_DIFF>), grid, dim3(256), 0, e->stream, s, src_stride,
-					   n, flist, fadd, fmul, e->rhist, out_g);
+					   div, ptrs, n, flist, fadd, fmul, e->rhist, out_g);
 		else
 			hipLaunchKernelGGL((select_rice_hist_kernel<4, PRE_NONE>), grid, dim3(256), 0, e->stream, s, src_stride,
-					   n, flist, fadd, fmul, e->rhist, out_g);
+					   div, ptrs, n, flist, fadd, fmul, e->rhist, out_g);
 	}
 	HIPCHECK(hipGetLastError());
 	return 0;
+}
+
+extern "C" uint32_t airs_dev_select_rice(struct airs_dev_engine *e, const void *src, uint64_t src_stride,
+					 uint32_t sample_bytes, uint32_t n, uint32_t num_frames,
+					 const uint32_t *flist, uint32_t fadd, uint32_t fmul, uint32_t preprocessing,
+					 uint32_t *out_g)
+{
+	return select_rice(e, src, src_stride, 1u, nullptr, sample_bytes, n, num_frames, flist, fadd, fmul,
+			   preprocessing, out_g);
 }
 
 extern "C" uint32_t airs_dev_fb_step(struct airs_dev_engine *e, const struct airs_fb_step *s)

@@ -40,10 +40,11 @@ enum cmp_gpu_sample_type {
 };
 
 /* flags */
-#define CMP_GPU_AUTO_RICE 0x1u /* GOLOMB_ZERO passes after NONE or DIFF preprocessing: choose
-				* g = 2^k per frame (k in [0,15], fewest payload bits, ties to
-				* smaller k) instead of the configured encoder parameter; IWT
-				* and MODEL passes keep theirs; build-defined extension */
+#define CMP_GPU_AUTO_RICE 0x1u /* GOLOMB_ZERO passes after NONE, DIFF or IWT preprocessing:
+				* choose g = 2^k per frame (k in [0,15], fewest payload bits
+				* for the pass's residuals -- the IWT coefficients for IWT --,
+				* ties to smaller k) instead of the configured encoder
+				* parameter; MODEL passes keep theirs; build-defined extension */
 #define CMP_GPU_HOST_STEPPED 0x2u /* batches that can fall back or fail: step the context state
 				   * machine on the host (one synchronisation per acquisition step)
 				   * instead of on the device; same output, for comparisons */

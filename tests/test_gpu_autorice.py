@@ -183,3 +183,73 @@ def test_autorice_model_batch(prod, eng, orc, orc_ext, kind, n, fallback, extra)
     assert got[1] == want[1]
     bad = [f for f in range(nctx * fpc) if got[0][f] != want[0][f]]
     assert not bad, f"frames {bad} differ"
+
+
+# IWT passes (round 5): k from the pass's residuals, the IWT coefficients.
+# The oracle side runs the IWT pass once to get them (its work buffer holds
+# the coefficients afterwards, preprocess.c:321-353), picks k with
+# orc_select_rice_k over them as 16-bit NONE residuals, then encodes with 2^k.
+IWT_CASES = [("u16", 65536, 0), ("u16", 1 << 20, 0), ("i16", 5000, 0), ("i16_in_i32", 70000, 0),
+             ("u16", 65536, 1), ("i16", 4160, 1)]
+
+
+@pytest.mark.parametrize("kind,n,fallback", IWT_CASES)
+def test_autorice_iwt_vs_oracle(prod, eng, orc, orc_ext, kind, n, fallback):
+    import torch
+    rng = np.random.default_rng(zlib.crc32(f"iwt/{kind}/{n}/{fallback}".encode()))
+    nf = int(max(2, min(12, (2 << 20) // n)))
+    frames = _frames(rng, kind, n, nf, extreme=True)
+    if fallback:  # a few noise frames that fall back
+        for f in range(0, nf, 3):
+            x = rng.integers(-32768, 32768, n)
+            frames[f] = (x & 0xFFFF).astype(np.uint16) if kind == "u16" else x.astype(
+                np.int16 if kind == "i16" else np.int32)
+    sb = 4 if kind == "i16_in_i32" else 2
+    wbs = (2 * n + 15) // 16 * 16
+    raw = 16 + 2 * n
+    want = []
+    for x in frames:
+        c0, wb = api.CmpContext(), api.aligned_empty(wbs)
+        prm = P(primary_preprocessing=api.PREPROCESS_IWT, primary_encoder_type=api.ENCODER_GOLOMB_ZERO,
+                primary_encoder_param=1)
+        assert not api.is_error(orc.initialise(c0, prm, wb, wbs))
+        cap = 6 * n + 64
+        d = api.aligned_empty(cap)
+        assert not api.is_error(orc.compress(kind, c0, d, cap, x))
+        k = orc_ext.orc_select_rice_k(wb.ctypes.data, n, 0, api.PREPROCESS_NONE, None)
+        c1, wb1 = api.CmpContext(), api.aligned_empty(wbs)
+        prm = P(primary_preprocessing=api.PREPROCESS_IWT, primary_encoder_type=api.ENCODER_GOLOMB_ZERO,
+                primary_encoder_param=1 << k, uncompressed_fallback_enabled=fallback)
+        assert not api.is_error(orc.initialise(c1, prm, wb1, wbs))
+        ocap = raw if fallback else cap
+        r = orc.compress(kind, c1, d, ocap, x)
+        assert not api.is_error(r), api.error_name(r)
+        want.append(bytes(d[:r]))
+    # the GPU: one context, nf acquisitions, AUTO_RICE (the configured g is ignored)
+    stride = (n * sb + 15) // 16 * 16
+    host = np.zeros(nf * stride, dtype=np.uint8)
+    for f, x in enumerate(frames):
+        host[f * stride:f * stride + n * sb] = np.ascontiguousarray(x).view(np.uint8)
+    src = torch.from_numpy(host).cuda()
+    cap = raw if fallback else 6 * n + 64
+    dstride = (6 * n + 64 + 7) // 8 * 8
+    dst = torch.full((nf * dstride,), 0xAB, dtype=torch.uint8, device="cuda")
+    sizes = torch.zeros(nf, dtype=torch.int32, device="cuda")
+    work = torch.zeros(wbs, dtype=torch.uint8, device="cuda")
+    ctxs = (api.CmpContext * 1)()
+    prm = P(primary_preprocessing=api.PREPROCESS_IWT, primary_encoder_type=api.ENCODER_GOLOMB_ZERO,
+            primary_encoder_param=7, uncompressed_fallback_enabled=fallback)
+    assert not api.is_error(prod.initialise(ctxs[0], prm, work.data_ptr(), wbs))
+    torch.cuda.synchronize()
+    r = eng.compress(ctxs, nf, kind, src.data_ptr(), stride, n * sb, dst.data_ptr(), dstride, cap,
+                     sizes.data_ptr(), 1)
+    assert r == 0, api.error_name(r)
+    assert eng.synchronize() == 0
+    sz = sizes.cpu().numpy().astype(np.uint32)
+    out = dst.cpu().numpy()
+    got = [bytes(out[f * dstride:f * dstride + int(sz[f])]) for f in range(nf)]
+    bad = [f for f in range(nf) if _mask(got[f]) != _mask(want[f])]
+    assert not bad, (f"frames {bad[:8]} differ; g gpu/oracle "
+                     f"{[(api.parse_header(got[f])['encoder_param'], api.parse_header(want[f])['encoder_param']) for f in bad[:4] if len(got[f]) >= 22]}")
+    if fallback:
+        assert any(api.parse_header(w)["encoder_type"] == api.ENCODER_UNCOMPRESSED for w in want)
