@@ -610,19 +610,17 @@ __global__ __launch_bounds__(64) void ck_chain_kernel(const uint8_t *src, uint64
 // orc_select_rice_k): total_k = n(k+1) + sum_i min(v_i >> k, 16), v = m + 1.
 // The 129-bin histogram of enc_common.h (auto_term) is a sufficient statistic.
 // ---------------------------------------------------------------------
-// Frames above AUTO_MAX_SPF segments (the fused path's limit), and MODEL
-// passes: a frame takes one workgroup per RICE_SLICE samples (a 4 Mi-sample
-// frame 64), which read its 4096-sample chunks interleaved.  Each workgroup
-// builds its histogram in LDS with
-// the fused path's layout (enc_kernel.h AUTO: the 129 bins of
+// Frames above AUTO_MAX_SPF segments (the fused path's limit), passes that
+// store a model, and IWT passes (over their coefficients): a frame takes one
+// workgroup per RICE_SLICE samples (a 4 Mi-sample frame 64), which read its
+// 4096-sample chunks interleaved.  Each workgroup builds its histogram in LDS
+// with the fused path's layout (enc_kernel.h AUTO: the 129 bins of
 // enc_common.h auto_term, one 32-bit counter per bin and lane, so a wave's
 // atomics never share a bank) and adds the non-zero bins to the frame's
-// global histogram; the workgroup that arrives last (a per-frame counter) takes
-// the argmin of the 16 totals, ties to the smaller k, and writes g.
-#ifndef AIRS_RICE_SLICE_CH // 4096-sample chunks per workgroup
-#define AIRS_RICE_SLICE_CH 16u
-#endif
-#define RICE_SLICE (256u * AIRS_PT * AIRS_RICE_SLICE_CH)
+// global histogram; the workgroup that arrives last (a per-frame counter)
+// takes the argmin of the 16 totals, ties to the smaller k, and writes g.
+// (4, 8 or 32 chunks per workgroup instead of 16 measured the same.)
+#define RICE_SLICE (256u * AIRS_PT * 16u)
 #define RICE_HSTRIDE 132u // global words per launch frame: 129 bins, the arrival counter, pad
 template <int W, int PRE>
 __global__ __launch_bounds__(256) void select_rice_hist_kernel(const uint8_t *src, uint64_t stride, uint32_t div,
@@ -645,12 +643,10 @@ __global__ __launch_bounds__(256) void select_rice_hist_kernel(const uint8_t *sr
 	// lane's counter of bin b at byte hbase + 256 (b + 1016): b from the float bits
 	const uint32_t hbase = (uint32_t)(uintptr_t)H + 4u * lane - 1016u * 256u;
 	__syncthreads();
-	// one 16-sample group per lane and step, the next step's loads in flight
-	// while this one is binned (the step count is uniform: the shuffle below
-	// needs every lane of the wave).  Workgroup y takes the frame's 4096-sample
-	// chunks y, y + G, y + 2G, ... (G = gridDim.y): at any time the frame's
-	// workgroups read one contiguous span, not G spans a slice apart (which
-	// crowd a few HBM channels)
+	// one 16-sample group per lane and step (the step count is uniform: the
+	// shuffle below needs every lane of the wave).  Workgroup y takes the
+	// frame's 4096-sample chunks y, y + G, y + 2G, ... (G = gridDim.y), so at
+	// any time the frame's workgroups read one contiguous span
 	const uint32_t G = gridDim.y;
 	constexpr uint32_t CHN = 256u * AIRS_PT; // samples per chunk
 	const uint32_t chunks = (n + CHN - 1u) / CHN, y = blockIdx.y;
