@@ -15,8 +15,10 @@
  * consecutive files of the same size (up to BATCH_BYTES) go to the GPU as
  * one cmp_gpu_compress() batch, which produces the same frames, in the same
  * order and with the same context state, as one cmp_compress_u16() per file
- * (cmp_gpu.h).  Parameter sets that need a work buffer (MODEL or IWT) keep
- * one host-API call per file, as the reference does (file.c:435-488).
+ * (cmp_gpu.h).  Parameter sets that need a work buffer (MODEL or IWT) batch
+ * the same way since round 5, with the work buffer on the device: the model
+ * carries from one file to the next, inside a batch and across batches, as
+ * in the reference's per-file loop (file.c:435-488).
  *
  * Decompression (the reference's default mode prints "Decompression not
  * implemented yet", airspacecli.c:421-423) is an extension here: the frames
@@ -405,39 +407,6 @@ static uint32_t frame_capacity(uint32_t src_size)
 	return cap;
 }
 
-/* one host-API call per file (parameter sets with a work buffer) */
-static int compress_one(struct job *j, struct cmp_context *ctx, int i)
-{
-	uint8_t *raw;
-	size_t size;
-	int owned, r = -1;
-	uint16_t *x;
-	uint8_t *dst;
-	uint32_t cap, got;
-
-	if (load_file(j->in[i], &raw, &size, &owned))
-		return -1;
-	if (size % 2u) {
-		log_msg(LOG_ERROR, "%s: file size not a multiple of 2", display(j->in[i]));
-		goto out;
-	}
-	x = xmalloc(size);
-	be16_to_host(x, raw, size / 2u);
-	cap = frame_capacity((uint32_t)size);
-	dst = xmalloc(cap);
-	got = cmp_compress_u16(ctx, dst, cap, x, (uint32_t)size);
-	if (cmp_is_error(got))
-		log_cmp(got, "Compression failed for %s", display(j->in[i]));
-	else
-		r = emit(j, i, dst, got, (uint32_t)size);
-	free(dst);
-	free(x);
-out:
-	if (owned)
-		free(raw);
-	return r;
-}
-
 /* A run of same-size files [i0, i1) as one GPU batch (frames at a 16-byte
  * stride in stage), written out in order. */
 static int compress_run(struct job *j, struct dev *d, struct cmp_context *ctx, int i0, int i1, uint32_t size,
@@ -516,19 +485,21 @@ static int compress_files(struct job *j, const struct cmp_params *par)
 		log_cmp(wbs, "Error calculating work buffer size");
 		return -1;
 	}
-	if (wbs)
-		wb = xmalloc(wbs);
+	if (wbs) {
+		/* the work buffer on the device (cmp_gpu_compress reads and writes it there) */
+		if (dev_open(&d) || hipMalloc(&wb, ((size_t)wbs + 15u) & ~(size_t)15u) != hipSuccess) {
+			log_msg(LOG_ERROR, "GPU allocation of the work buffer failed");
+			wb = NULL;
+			goto done;
+		}
+	}
 	e = cmp_initialise(&ctx, par, wb, wbs);
 	if (cmp_is_error(e)) {
 		log_cmp(e, "Compression initialization failed");
 		goto done;
 	}
 
-	if (wbs) {
-		for (i = 0; i < j->n_in; i++)
-			if (compress_one(j, &ctx, i))
-				goto done;
-	} else {
+	{
 		/* batches of consecutive same-size files */
 		uint16_t *stage = NULL;
 		size_t stage_cap = 0;
@@ -593,8 +564,9 @@ static int compress_files(struct job *j, const struct cmp_params *par)
 	log_summary("compressed", j->in, j->n_in, j->sum_in, j->last_out ? j->last_out : "", j->sum_out);
 	r = 0;
 done:
+	if (wb)
+		hipFree(wb);
 	dev_close(&d);
-	free(wb);
 	return r;
 }
 

@@ -165,6 +165,12 @@ PARAMS = {
                 primary_encoder_outlier=100),
     "fallback": dict(primary_preprocessing=0, primary_encoder_type=1, primary_encoder_param=1,
                      uncompressed_fallback_enabled=1),
+    # IWT primaries, MODEL secondaries and the fallback: the device work buffer
+    # carries the model through the batch (round 5: these sets batch too)
+    "iwt_model_fb": dict(primary_preprocessing=2, primary_encoder_type=1, primary_encoder_param=16,
+                         secondary_iterations=2, secondary_preprocessing=3, secondary_encoder_type=1,
+                         secondary_encoder_param=8, model_rate=7, uncompressed_fallback_enabled=1,
+                         checksum_enabled=1),
 }
 
 
@@ -180,7 +186,7 @@ def sample_files(d, kind, rng):
     """Seven files: four of 5000 samples, two of 777, one of 5000 (runs of equal
     size, so the batched path splits), or all 3000 for parameter sets with a
     work buffer."""
-    sizes = [3000] * 6 if kind in ("model_chain", "iwt") else [5000, 5000, 5000, 5000, 777, 777, 5000]
+    sizes = [3000] * 6 if kind in ("model_chain", "iwt", "iwt_model_fb") else [5000, 5000, 5000, 5000, 777, 777, 5000]
     base = np.cumsum(rng.integers(-200, 200, max(sizes)))
     paths, xs = [], []
     for i, n in enumerate(sizes):
