@@ -454,3 +454,17 @@ int airs_dev_commit_release(struct airs_dev_engine *e, uint32_t seq, const uint6
 	(void)total;
 	return 0; /* the caller patches */
 }
+
+/* the gather's identifier patch: six big-endian bytes at data + offsets[i] + 8 */
+uint32_t airs_dev_patch_ids_at(struct airs_dev_engine *e, void *data, const uint64_t *offsets, const uint64_t *ids,
+			       uint64_t n)
+{
+	uint64_t i;
+	int b;
+
+	(void)e;
+	for (i = 0; i < n; i++)
+		for (b = 0; b < 6; b++)
+			((uint8_t *)data)[offsets[i] + 8u + (uint64_t)b] = (uint8_t)(ids[i] >> (8 * (5 - b)));
+	return 0;
+}

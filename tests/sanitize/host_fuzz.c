@@ -231,6 +231,43 @@ static void fuzz_params_parse(void)
 	(void)cmp_params_to_string(out, pick(2) ? sizeof(out) : pick(40), &p);
 }
 
+/* cmp_gpu_gather_plan (cmp_gather.c): random node tables, every layout,
+ * error values, frames without draws; outputs checked for shape */
+static uint32_t n_plan_ok, n_plan_refused;
+static void fuzz_gather_plan(void)
+{
+	const uint32_t world = 1u + rnd() % 8u, F = 1u + rnd() % 12u, layout = rnd() % 4u;
+	const uint32_t fpc = 1u + rnd() % 4u, total = world * F;
+	uint64_t *entries = malloc(total * 8u), *rank_bytes = malloc(world * 8u), *offsets = malloc(total * 8u);
+	uint64_t *ids = malloc(total * 8u), sum = 0;
+	uint32_t *sizes = malloc(total * 4u), i, r;
+
+	for (i = 0; i < total; i++) {
+		uint64_t sz = rnd() % 5000u, dr = rnd() % 4u;
+
+		if (rnd() % 64u == 0u)
+			sz = (uint64_t)(0u - 5u); /* an error value in a size slot */
+		entries[i] = sz | dr << 32;
+	}
+	r = cmp_gpu_gather_plan(entries, world, F, layout, fpc, rnd(), rank_bytes, offsets, sizes,
+				rnd() % 2u ? ids : NULL);
+	if (cmp_is_error(r)) {
+		n_plan_refused++;
+	} else {
+		n_plan_ok++;
+		for (i = 0; i < world; i++)
+			sum += rank_bytes[i];
+		for (i = 0; i < total; i++)
+			if ((offsets[i] & 7u) || offsets[i] + sizes[i] > sum)
+				abort();
+	}
+	free(entries);
+	free(rank_bytes);
+	free(offsets);
+	free(ids);
+	free(sizes);
+}
+
 int main(int argc, char **argv)
 {
 	const uint32_t iters = argc > 1 ? (uint32_t)strtoul(argv[1], NULL, 0) : 3000u;
@@ -247,8 +284,10 @@ int main(int argc, char **argv)
 		fuzz_host_api();
 		fuzz_batch(eng);
 		fuzz_params_parse();
+		fuzz_gather_plan();
 	}
 	cmp_gpu_engine_destroy(eng);
+	printf("gather plans: %u ok, %u refused\n", n_plan_ok, n_plan_refused);
 	printf("host_fuzz: %u iterations clean: %u contexts initialised, host frames %u ok / %u errors, "
 	       "%u batches (%u frames ok, %u with fallback enabled), %u streams, %lu walks\n",
 	       iters, n_init_ok, n_frames_ok, n_frames_err, n_batch_ok, n_batch_frames_ok, n_batch_fallback_cap,
