@@ -213,6 +213,12 @@ uint32_t airs_dev_synth(struct airs_dev_engine *e, void *dst, uint32_t sample_by
 		       * placement, checksum products, decoder parse arrays, decoder frame info, IWT heads) */
 #define AIRS_SLOT_GATHER 11 /* slots 11..13: cmp_gpu_gather (cmp_gather.c); 0..10 cmp_host.c */
 void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes);
+/* engine-owned device words for the gather's status exchanges (cmp_gather.c),
+ * allocated with the engine so that taking part in an exchange never needs an
+ * allocation that could fail on one rank only: 2 words in, then
+ * 2 * AIRS_COLL_MAX_RANKS words out */
+#define AIRS_COLL_MAX_RANKS 256
+uint64_t *airs_dev_coll(struct airs_dev_engine *e);
 /* engine-owned page-locked host scratch, grown on demand: asynchronous
  * read-backs and uploads; the host may rewrite it once the stream has passed
  * the copies that use it */

@@ -70,7 +70,8 @@ struct KArgs {
 	uint64_t *tail;  // per segment: epoch << 32 | last 32 bits of the segment's stream
 	uint32_t *ticket;
 	uint64_t src_stride, dst_stride, model_stride;
-	uint32_t frame_add, frame_mul, model_div, pad0;
+	uint32_t frame_add, frame_mul, model_div;
+	uint32_t lbmode; // rice_kernel: bit 0 = every segment and its predecessors on one XCD (scalar look-back polls)
 	uint64_t id_base, id_step, fail_bit;
 	uint32_t n, segs_per_frame, num_segs, cap;
 	uint32_t g, outlier_param;
@@ -454,6 +455,21 @@ __device__ __forceinline__ uint32_t gt16_mask(uint32_t q)
 // rounds | retries << 32, 6 tail re-polls; slot 7 = HW_ID << 32 | XCC_ID.  scripts/ts_analyze.py.
 __device__ __forceinline__ void dbg_stamp(const KArgs &a, uint32_t gseg, uint32_t slot)
 {
+	if (DBG(131072u)) { // light timeline: slots 0 and 4 only, with the shader clock in 1 and 2
+		if (DBG(65536u) && a.dbgts && threadIdx.x == 0 && (slot == 0 || slot == 4)) {
+			uint64_t t, c;
+			asm volatile("s_memrealtime %0\n s_memtime %1\n s_waitcnt lgkmcnt(0)" : "=s"(t), "=s"(c));
+			a.dbgts[8u * gseg + slot] = t;
+			a.dbgts[8u * gseg + (slot ? 2u : 1u)] = c;
+			if (slot == 0) {
+				uint32_t hw, xcc;
+				asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+				asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+				a.dbgts[8u * gseg + 7u] = ((uint64_t)hw << 32) | xcc;
+			}
+		}
+		return;
+	}
 	if (DBG(65536u) && a.dbgts && threadIdx.x == 0) {
 		uint64_t t;
 		asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t));

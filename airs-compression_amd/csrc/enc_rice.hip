@@ -34,6 +34,7 @@
 // bounded spins are those of encode_kernel.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "enc_common.h"
 
@@ -259,6 +260,127 @@ __device__ __forceinline__ uint2 rice_lookback(const KArgs &a, uint32_t gseg, ui
 		tv = gran_load(&a.tail[gseg - 1u]);
 	}
 	return lb_resolve(a, gseg, sif, lane, gv, tv, rounds);
+}
+
+// The look-back on scalar loads only (lbmode bit 0: a frame's segments all
+// run on one XCD, so its L2 holds every granule the frame's segments write
+// and a scalar load that misses the scalar cache sees the newest value).
+// A vector poll queues behind the CU's sample loads (~2.4 us per re-poll on
+// a loaded CU); a scalar poll does not (~1 us).  Windows of
+// 16 granules, newest first, evaluated in scalar code: granules are summed
+// down to the nearest inclusive one; an unpublished granule is re-polled
+// after s_sleep, with the sum of the newer ones kept; a window of aggregates
+// only moves on to the next one at once.  After AIRS_RICE_SPOLL polls the
+// vector look-back takes over (liveness whatever the placement).  sif >= 16.
+#ifndef AIRS_RICE_SPOLL
+#define AIRS_RICE_SPOLL 4096u
+#endif
+#ifndef AIRS_RICE_SWIN // granules per scalar window (8: one s_load_dwordx16; 16: two)
+#define AIRS_RICE_SWIN 16
+#endif
+__device__ __forceinline__ uint2 rice_lookback_s(const KArgs &a, uint32_t gseg, uint32_t sif, uint32_t lane)
+{
+	typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+	constexpr uint32_t SW = AIRS_RICE_SWIN;
+	auto sptr = [](const uint64_t *p) {
+		const uint64_t v = (uint64_t)(uintptr_t)p;
+		const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)v);
+		const uint32_t h = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+		return (const uint64_t *)(uintptr_t)(((uint64_t)h << 32) | l);
+	};
+	const uint32_t first_seg = gseg - sif, epoch = a.epoch;
+	uint32_t sum = 0u, polls = 0u, rounds = 0u, j = gseg - 1u;
+	uint64_t tv = 0ull;
+	bool have_tail = false, done = false;
+	while (polls < AIRS_RICE_SPOLL) {
+		const uint32_t base = j >= first_seg + (SW - 1u) ? j - (SW - 1u) : first_seg;
+		const uint64_t *gp = sptr(&a.agg[base]);
+		u32x16 q[SW / 8u];
+		if (!have_tail) {
+			const uint64_t *tp = sptr(&a.tail[gseg - 1u]);
+			if constexpr (SW == 16u)
+				asm volatile("s_load_dwordx16 %0, %3, 0x0 glc\n\t"
+					     "s_load_dwordx16 %1, %3, 0x40 glc\n\t"
+					     "s_load_dwordx2 %2, %4, 0x0 glc\n\t"
+					     "s_waitcnt lgkmcnt(0)"
+					     : "=&s"(q[0]), "=&s"(q[SW / 8u - 1u]), "=&s"(tv)
+					     : "s"(gp), "s"(tp)
+					     : "memory");
+			else
+				asm volatile("s_load_dwordx16 %0, %2, 0x0 glc\n\t"
+					     "s_load_dwordx2 %1, %3, 0x0 glc\n\t"
+					     "s_waitcnt lgkmcnt(0)"
+					     : "=&s"(q[0]), "=&s"(tv)
+					     : "s"(gp), "s"(tp)
+					     : "memory");
+			have_tail = (uint32_t)(tv >> 32) == epoch;
+		} else {
+			if constexpr (SW == 16u)
+				asm volatile("s_load_dwordx16 %0, %2, 0x0 glc\n\t"
+					     "s_load_dwordx16 %1, %2, 0x40 glc\n\t"
+					     "s_waitcnt lgkmcnt(0)"
+					     : "=&s"(q[0]), "=&s"(q[SW / 8u - 1u])
+					     : "s"(gp)
+					     : "memory");
+			else
+				asm volatile("s_load_dwordx16 %0, %1, 0x0 glc\n\t"
+					     "s_waitcnt lgkmcnt(0)"
+					     : "=&s"(q[0])
+					     : "s"(gp)
+					     : "memory");
+		}
+		rounds++;
+		// newest first: 0 = every granule an aggregate, 1 = inclusive found,
+		// 2 = granule `j` unpublished
+		uint32_t stop = 0u;
+#pragma unroll
+		for (int i = (int)SW - 1; i >= 0; i--) {
+			const uint32_t lo = q[i >> 3][2 * (i & 7)], hi = q[i >> 3][2 * (i & 7) + 1];
+			if (stop == 0u && base + (uint32_t)i <= j) {
+				if ((hi >> 1) != epoch) {
+					stop = 2u;
+					j = base + (uint32_t)i;
+				} else {
+					sum += lo;
+					stop = hi & 1u;
+				}
+			}
+		}
+		if (stop == 1u) {
+			done = true;
+			break;
+		}
+		if (stop == 0u) {
+			if (base == first_seg) // never: the frame's first granule is inclusive
+				break;
+			j = base - 1u;
+			continue;
+		}
+		polls++;
+		__builtin_amdgcn_s_sleep(1);
+	}
+	// the predecessor's tail
+	while (done && !have_tail && polls < AIRS_RICE_SPOLL) {
+		const uint64_t *tp = sptr(&a.tail[gseg - 1u]);
+		polls++;
+		__builtin_amdgcn_s_sleep(1);
+		asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\t"
+			     "s_waitcnt lgkmcnt(0)"
+			     : "=&s"(tv)
+			     : "s"(tp)
+			     : "memory");
+		have_tail = (uint32_t)(tv >> 32) == epoch;
+	}
+	if (DBG(65536u) && a.dbgts && lane == 0) {
+		a.dbgts[8u * gseg + 5u] = ((uint64_t)polls << 32) | rounds;
+		a.dbgts[8u * gseg + 6u] = 0u;
+	}
+	if (done && have_tail)
+		return make_uint2(sum, (uint32_t)tv);
+	// the vector look-back from the start (never expected on one XCD)
+	const int64_t idx = (int64_t)gseg - 1 - (int64_t)lane;
+	const uint64_t gv = gran_load(&a.agg[idx >= (int64_t)first_seg ? idx : (int64_t)first_seg]);
+	return lb_resolve(a, gseg, sif, lane, gv, gran_load(&a.tail[gseg - 1u]), rounds);
 }
 
 // Store `tot` bits of an LDS image (bit 0 of word 0 = bit Pc of the frame)
@@ -553,7 +675,8 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 				if (DBG(2u)) // ablation: no look-back (offsets invented, output garbage)
 					pp = make_uint2(HDR_BITS + sif * 37u, 0u);
 				else if (!is_first)
-					pp = rice_lookback(a, gseg, sif, lane, 0ull);
+					pp = (a.lbmode & 1u) && sif >= 16u ? rice_lookback_s(a, gseg, sif, lane)
+									     : rice_lookback(a, gseg, sif, lane, 0ull);
 				if (lane == 0) {
 					if (!is_first)
 						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (pp.x + A));
@@ -583,7 +706,8 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		if (wid == 0) {
 			uint2 pp = make_uint2(HDR_BITS, hdr_pred);
 			if (!is_first)
-				pp = rice_lookback(a, gseg, sif, lane, 0ull);
+				pp = (a.lbmode & 1u) && sif >= 16u ? rice_lookback_s(a, gseg, sif, lane)
+								     : rice_lookback(a, gseg, sif, lane, 0ull);
 			if (lane == 0) {
 				if (!is_first)
 					gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (pp.x + A));
@@ -686,6 +810,15 @@ bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s, bool stream)
 	ka.segs_per_frame = k.n / RSEGN;
 	ka.num_segs = nfr * ka.segs_per_frame;
 	ka.img_words = rice_arena_words();
+	// block b runs on XCD b mod 8 (round-robin placement, MI355X_MICROARCH.md):
+	// with the frame-interleaved order, segment d and its predecessor d - nfr
+	// share an XCD when nfr is a multiple of 8 (speed only: every poll's
+	// value is true wherever it runs, and the vector look-back takes over
+	// after AIRS_RICE_SPOLL scalar polls)
+	ka.lbmode = !stream && nfr % 8u == 0u ? 1u : 0u;
+	static const char *lbm = getenv("AIRS_RICE_LBMODE"); // benchmarking override
+	if (lbm)
+		ka.lbmode = (uint32_t)atoi(lbm);
 	const size_t lds = (size_t)ka.img_words * 4u;
 	void (*kern)(KArgs);
 	if (stream)

@@ -1104,10 +1104,17 @@ static thread_local char g_err[256];
 // (scripts/kbench.py) through this entry point; the product build has none.
 static uint32_t g_dbg;
 static char g_dbgts_path[512];
+// AIRS_DBGTS_RING=R: the timeline keeps the last R launches (slot = launch
+// number mod R, one block of 8 stamps per segment each), zeroed once at
+// allocation so that back-to-back launches see no extra memset
+static uint32_t g_dbgts_ring = 1u, g_dbgts_launch;
 extern "C" void airs_dev_set_debug(uint32_t bits, const char *timeline_path)
 {
 	g_dbg = bits;
 	snprintf(g_dbgts_path, sizeof(g_dbgts_path), "%s", timeline_path ? timeline_path : "");
+	const char *r = getenv("AIRS_DBGTS_RING");
+	g_dbgts_ring = r && atoi(r) > 0 ? (uint32_t)atoi(r) : 1u;
+	g_dbgts_launch = 0u;
 }
 #endif
 
@@ -1196,7 +1203,9 @@ extern "C" struct airs_dev_engine *airs_dev_engine_create(void *stream)
 	if (!e)
 		return nullptr;
 	e->stream = (hipStream_t)stream;
-	if (hipMalloc(&e->ticket, 256) != hipSuccess || hipMemset(e->ticket, 0, 256) != hipSuccess) {
+	// 256 bytes of tickets and fault words, then the gather's status words
+	const size_t tbytes = 256u + 16u * (AIRS_COLL_MAX_RANKS + 1u);
+	if (hipMalloc(&e->ticket, tbytes) != hipSuccess || hipMemset(e->ticket, 0, tbytes) != hipSuccess) {
 		free(e);
 		return nullptr;
 	}
@@ -1256,6 +1265,11 @@ extern "C" void *airs_dev_host_scratch(struct airs_dev_engine *e, size_t bytes)
 extern "C" void *airs_dev_engine_stream(struct airs_dev_engine *e)
 {
 	return e ? (void *)e->stream : nullptr;
+}
+
+extern "C" uint64_t *airs_dev_coll(struct airs_dev_engine *e)
+{
+	return e ? reinterpret_cast<uint64_t *>(e->ticket + 64) : nullptr;
 }
 
 extern "C" void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes)
@@ -1645,14 +1659,16 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 #if AIRS_ABLATE
 	k.dbg = g_dbg;
 	if (g_dbg & 65536) {
-		if (e->dbgts_n < 8u * segs) {
+		if (e->dbgts_n < 8u * segs * g_dbgts_ring) {
 			(void)hipFree(e->dbgts);
-			e->dbgts_n = 8u * segs;
+			e->dbgts_n = 8u * segs * g_dbgts_ring;
 			if (hipMalloc(&e->dbgts, e->dbgts_n * 8u) != hipSuccess)
 				return ERRV(E_GENERIC);
+			HIPCHECK(hipMemset(e->dbgts, 0, e->dbgts_n * 8u));
 		}
-		HIPCHECK(hipMemsetAsync(e->dbgts, 0, 8u * segs * 8u, e->stream));
-		k.dbgts = e->dbgts;
+		if (g_dbgts_ring == 1u)
+			HIPCHECK(hipMemsetAsync(e->dbgts, 0, 8u * segs * 8u, e->stream));
+		k.dbgts = e->dbgts + 8u * segs * (g_dbgts_launch++ % g_dbgts_ring);
 	}
 #endif
 

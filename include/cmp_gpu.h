@@ -202,8 +202,15 @@ uint32_t cmp_gpu_pack_frames(struct cmp_gpu_engine *engine, const void *frames, 
  * secondary pass depends on its rank's previous frame: use STREAMS).  Every
  * rank decides from the same all-gathered table, so all ranks return the same
  * refusal; a frame with an error value is refused the same way
- * (CMP_ERR_GENERIC).  RCCL is loaded on first use.  The transfers are queued
- * on the engine's stream; cmp_gpu_synchronize waits for them.  Build-defined
+ * (CMP_ERR_GENERIC), and so is a root out_capacity below the packed bytes
+ * (CMP_ERR_DST_TOO_SMALL).  Local failures on any rank (NULL frames / sizes,
+ * the root's NULL or misaligned out, an allocation, the packing) are shared
+ * through two status exchanges before the next collective, so every rank
+ * returns the same value and no rank is left waiting in RCCL.  A NULL engine
+ * or communicator, or a world above 256 ranks, cannot take part and returns
+ * CMP_ERR_GENERIC at once (a caller error on every rank alike).  RCCL is the
+ * copy the process already holds, else loaded on first use.  When the call
+ * returns, the transfers and the identifier patch are complete.  Build-defined
  * extension (the C form of airs-compression_amd/shard.py).
  */
 enum cmp_gpu_layout { CMP_GPU_LAYOUT_ROUNDROBIN = 0, CMP_GPU_LAYOUT_BLOCK = 1, CMP_GPU_LAYOUT_STREAMS = 2 };

@@ -48,7 +48,15 @@ flags = 1 if (wl.get("auto_rice") or os.environ.get("AIRS_KB_AUTO")) else 0
 for k in range(10):
     assert eng.compress(ctxs, nf, "u16", src.data_ptr(), stride, stride, dst.data_ptr(), dstride, cap,
                         sizes.data_ptr(), flags) == 0
+# AIRS_KB_PRE=P: P more untimed launches over the rotated (cold) sets before
+# the timed spans; AIRS_KB_IDLE=MS: then leave the GPU idle for MS ms
+for k in range(int(os.environ.get("AIRS_KB_PRE", "0"))):
+    assert eng.compress(ctxs, nf, "u16", srcs[k % ROT].data_ptr(), stride, stride, dsts[k % ROT].data_ptr(), dstride,
+                        cap, sizes.data_ptr(), flags) == 0
 torch.cuda.synchronize()
+if os.environ.get("AIRS_KB_IDLE"):
+    import time
+    time.sleep(float(os.environ["AIRS_KB_IDLE"]) / 1e3)
 ms = []
 for rep in range(5):  # 5 spans of 20 back-to-back launches, one event pair each
     e0 = torch.cuda.Event(enable_timing=True)

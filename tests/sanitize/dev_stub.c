@@ -24,7 +24,17 @@ struct airs_dev_engine {
 	void *pinned;
 	size_t pinned_cap;
 	uint64_t salt;
+	uint64_t coll[2 + 2 * AIRS_COLL_MAX_RANKS];
 };
+
+/* failure injection for the multi-rank gather harness (gather_sim.c): the
+ * scratch slot whose allocation fails on this thread (-1: none) */
+__thread int stub_scratch_fail_slot = -1;
+
+uint64_t *airs_dev_coll(struct airs_dev_engine *e)
+{
+	return e ? e->coll : NULL;
+}
 
 static uint64_t mix(uint64_t z)
 {
@@ -78,7 +88,7 @@ void *airs_dev_engine_stream(struct airs_dev_engine *e)
 
 void *airs_dev_scratch(struct airs_dev_engine *e, int slot, size_t bytes)
 {
-	if (!e || slot < 0 || slot >= AIRS_NSLOT)
+	if (!e || slot < 0 || slot >= AIRS_NSLOT || slot == stub_scratch_fail_slot)
 		return NULL;
 	if (bytes > e->cap[slot]) {
 		free(e->scratch[slot]);

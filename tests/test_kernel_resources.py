@@ -21,8 +21,11 @@ LIB = os.path.join(PKG_DIR, "lib", "libairscmp.so")
 BUDGETS = {
     # cfg2 / cfg4: the Rice/ZERO frame kernel (enc_rice.hip), DIFF and NONE:
     # five waves per SIMD at <= 96 VGPRs
-    "_ZN4airs11rice_kernelILi1ELb0EEEvNS_5KArgsE": (96, 0),
-    "_ZN4airs11rice_kernelILi0ELb0EEEvNS_5KArgsE": (96, 0),
+    # (round 6: the scalar look-back of XCD-local frames, rice_lookback_s,
+    # holds a 16-granule window in 32 SGPRs: 19 spills to VGPR lanes, all in
+    # wave 0's look-back, once per segment)
+    "_ZN4airs11rice_kernelILi1ELb0EEEvNS_5KArgsE": (96, 24),
+    "_ZN4airs11rice_kernelILi0ELb0EEEvNS_5KArgsE": (96, 24),
     "_ZN4airs11rice_kernelILi1ELb1EEEvNS_5KArgsE": (96, 0),
     # encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>: frames the Rice
     # kernel does not take (k > 7, holes in device-planned launch lists); no
