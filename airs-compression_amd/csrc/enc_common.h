@@ -30,6 +30,8 @@
 #define AIRS_HCO_SEQ 1            // word: the commit kernel's signal (its sequence number)
 #define AIRS_HCO_GO 2             // word: the host's release of that kernel (the same number)
 #define AIRS_HCO_MODE 3           // word: 1 = patch the identifiers, 0 = not
+#define AIRS_HCO_ACK 4            // word: the commit kernel's acknowledgement, written when it
+                                  // has finished: (seq & 0x7FFFFFFF) << 1 | 1 if it patched
 #define AIRS_HCO_FLAGS 64         // byte offset of the per-context flags
 #define AIRS_HCO_MAX_CTX 8192u    // flags for up to this many contexts
 #define AIRS_HCO_IDS (64u + 8192u) // byte offset of the identifiers
@@ -96,6 +98,10 @@ struct KArgs {
 // per lane); larger frames take the sliced selection (select_rice_hist_kernel) first
 #ifndef AUTO_MAX_SPF
 #define AUTO_MAX_SPF 32u
+#endif
+// ... on engines not marked CMP_GPU_OPT_EXCLUSIVE (the GPU may be shared)
+#ifndef AUTO_SHARED_MAX_SPF
+#define AUTO_SHARED_MAX_SPF 8u
 #endif
 // histogram bins: v = m + 1 in [1, 65536], bin = 8 floor(log2 v) + next 3 bits
 #define AUTO_BINS 129u

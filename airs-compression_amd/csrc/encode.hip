@@ -759,6 +759,14 @@ __global__ __launch_bounds__(256) void select_rice_hist_kernel(const uint8_t *sr
 	// workgroup at four per CU).  Each bin add returns before the barrier, the
 	// arrival add after it; the last arrival reads the bins by exchanges, also
 	// at the memory side (an add of 0 may be turned into a cached load).
+	// This ordering is the hardware's, not the memory model's: relaxed
+	// atomics promise none.  It holds on gfx950 (returning agent-scope
+	// atomics are performed at the memory side in the order the wave waits
+	// for them); any other target must add release/acquire here first
+	// (ADVICE r5), hence the guard below.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "select_rice_hist_kernel's fence-free hand-off is verified for gfx950 only"
+#endif
 	uint32_t *gh = ghist + (uint64_t)blockIdx.x * RICE_HSTRIDE;
 	if (tid < AUTO_BINS && s_bin[tid]) {
 		const uint32_t r = __hip_atomic_fetch_add(&gh[tid], s_bin[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1005,12 +1013,15 @@ __global__ void patch_ids_kernel(uint8_t *dst, uint64_t stride, uint32_t num, ui
 // The speculative walk's commit (airs_dev_commit_*), one workgroup: flags[c]
 // = 1 when a frame of context c (frames c*fpc ..) has an error status, the
 // fault count, then (after a system-scope fence) the signal `seq`.  Then it
-// waits for the host's release (bounded: ~1 s of the 100 MHz clock) and, if
-// the release says so, writes the identifiers the host put in the block into
-// the headers of the frames without an error (as patch_ids_kernel).  The
-// stream's next work waits behind it, and no host launch is needed.
+// waits for the host's release (bounded: `ticks` of the 100 MHz clock, ~1 s)
+// and, if the release says so, writes the identifiers the host put in the
+// block into the headers of the frames without an error (as
+// patch_ids_kernel).  Last, its acknowledgement: whether it patched, so that
+// a host whose release came after the kernel gave up patches the headers
+// itself.  The stream's next work waits behind it, and no host
+// launch is needed.
 __global__ void commit_kernel(const uint32_t *status, uint32_t num_ctx, uint32_t fpc, const uint32_t *ticket,
-			      volatile uint32_t *hco, uint32_t seq, uint8_t *dst, uint64_t dst_stride)
+			      volatile uint32_t *hco, uint32_t seq, uint8_t *dst, uint64_t dst_stride, uint64_t ticks)
 {
 	__shared__ uint32_t s_mode;
 	volatile uint8_t *flags = reinterpret_cast<volatile uint8_t *>(hco) + AIRS_HCO_FLAGS;
@@ -1032,15 +1043,20 @@ __global__ void commit_kernel(const uint32_t *status, uint32_t num_ctx, uint32_t
 				mode = hco[AIRS_HCO_MODE];
 				break;
 			}
-			if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull)
+			if (__builtin_amdgcn_s_memrealtime() - t0 > ticks)
 				break; // no release: leave the headers alone
 			__builtin_amdgcn_s_sleep(8);
 		}
 		s_mode = mode;
 	}
 	__syncthreads();
-	if (s_mode != 1u)
+	if (s_mode != 1u) {
+		if (threadIdx.x == 0) {
+			__threadfence_system();
+			hco[AIRS_HCO_ACK] = (seq & 0x7FFFFFFFu) << 1;
+		}
 		return;
+	}
 	const volatile uint64_t *ids =
 		reinterpret_cast<const volatile uint64_t *>(reinterpret_cast<volatile uint8_t *>(hco) + AIRS_HCO_IDS);
 	const uint32_t total = num_ctx * fpc;
@@ -1051,6 +1067,11 @@ __global__ void commit_kernel(const uint32_t *status, uint32_t num_ctx, uint32_t
 		const uint64_t id = ids[f];
 		for (int b = 0; b < 6; b++)
 			p[b] = (uint8_t)(id >> (40 - 8 * b));
+	}
+	__syncthreads(); // every header written (the fence below covers the block's stores)
+	if (threadIdx.x == 0) {
+		__threadfence_system();
+		hco[AIRS_HCO_ACK] = ((seq & 0x7FFFFFFFu) << 1) | 1u;
 	}
 }
 
@@ -1153,6 +1174,9 @@ struct airs_dev_engine {
 	size_t pinned_cap;
 	volatile uint32_t *hco; // coherent page-locked block (AIRS_HCO_*), written in-stream
 	uint32_t hco_seq;       // the last sequence word asked for
+	uint32_t hco_released;  // the last sequence word released (airs_dev_commit_release)
+	uint64_t commit_ticks;  // the commit kernel's wait for the release (100 MHz ticks)
+	uint64_t commit_polls;  // the host's wait for the commit kernel's signal (pause loops)
 	// cmp_gpu_engine_set_option (include/cmp_gpu.h)
 	uint32_t opt_exclusive;     // CMP_GPU_OPT_EXCLUSIVE
 	uint32_t opt_walk_segment;  // CMP_GPU_OPT_WALK_SEGMENT: 0, 2048 or 4096
@@ -1216,7 +1240,16 @@ extern "C" struct airs_dev_engine *airs_dev_engine_create(void *stream)
 		return nullptr;
 	}
 	e->hco = (volatile uint32_t *)hf;
+	// the commit handshake's bounds; AIRS_TEST_COMMIT_TICKS / _POLLS shorten
+	// them to force its give-up paths (tests only)
+	e->commit_ticks = 100000000ull;
+	e->commit_polls = 1ull << 26;
+	if (const char *t = getenv("AIRS_TEST_COMMIT_TICKS"))
+		e->commit_ticks = strtoull(t, nullptr, 10);
+	if (const char *t = getenv("AIRS_TEST_COMMIT_POLLS"))
+		e->commit_polls = strtoull(t, nullptr, 10);
 	e->hco[AIRS_HCO_FAULT] = 0u;
+	e->hco[AIRS_HCO_ACK] = 0u;
 	e->hco[AIRS_HCO_SEQ] = 0u;
 	e->hco[AIRS_HCO_GO] = 0u;
 	e->epoch = 0;
@@ -1573,10 +1606,16 @@ extern "C" uint32_t airs_dev_encode(struct airs_dev_engine *e, const struct airs
 	if (r)
 		return r;
 	// CMP_GPU_AUTO_RICE: fused into the encode kernel for frames of a few
-	// segments without a model; otherwise the sliced selection writes g first
+	// segments without a model; otherwise the sliced selection writes g first.
+	// A fused segment waits at its frame's candidate barrier for LATER blocks
+	// of its frame (spf of the 128 workgroup slots of its XCD): on an engine
+	// that may share the GPU only frames of up to AUTO_SHARED_MAX_SPF segments,
+	// so that a kernel on another stream would have to hold all but a few of
+	// an XCD's slots to delay the barrier
+	const uint32_t auto_spf_max = e->opt_exclusive ? AUTO_MAX_SPF : AUTO_SHARED_MAX_SPF;
 	const bool auto_fused = L->auto_rice && L->encoder_type == ENC_ZERO &&
 				L->model_mode == AIRS_MODEL_NONE &&
-				(L->preprocessing == PRE_NONE || L->preprocessing == PRE_DIFF) && spf <= AUTO_MAX_SPF;
+				(L->preprocessing == PRE_NONE || L->preprocessing == PRE_DIFF) && spf <= auto_spf_max;
 	const uint32_t *frame_g = L->frame_g;
 	bool iwt_done = false;
 	if (L->auto_rice && !auto_fused && L->encoder_type == ENC_ZERO) {
@@ -2173,7 +2212,7 @@ extern "C" uint32_t airs_dev_commit_begin(struct airs_dev_engine *e, const uint3
 		return ERRV(E_PARAMS_INVALID);
 	*seq = ++e->hco_seq;
 	hipLaunchKernelGGL(commit_kernel, dim3(1), dim3(256), 0, e->stream, status, num_ctx, fpc, e->ticket, e->hco, *seq,
-			   (uint8_t *)dst, dst_stride);
+			   (uint8_t *)dst, dst_stride, e->commit_ticks);
 	HIPCHECK(hipGetLastError());
 	return 0;
 }
@@ -2184,7 +2223,7 @@ extern "C" uint32_t airs_dev_commit_begin(struct airs_dev_engine *e, const uint3
 // the release so that the kernel is not left waiting)
 extern "C" uint32_t airs_dev_commit_wait(struct airs_dev_engine *e, uint32_t seq, uint32_t num_ctx, uint8_t *flags)
 {
-	for (uint64_t i = 0; i < (1ull << 26); i++) { // ~ a second of polls
+	for (uint64_t i = 0; i < e->commit_polls; i++) { // ~ a second of polls
 		if (e->hco[AIRS_HCO_SEQ] == seq) {
 			const uint32_t faults = e->hco[AIRS_HCO_FAULT];
 			memcpy(flags, (const void *)((const volatile uint8_t *)e->hco + AIRS_HCO_FLAGS), num_ctx);
@@ -2209,8 +2248,16 @@ extern "C" uint32_t airs_dev_commit_wait(struct airs_dev_engine *e, uint32_t seq
 	return 0;
 }
 
+// Release the commit kernel of `seq`: 1 when it patched the identifiers
+// (ids given, and the kernel acknowledged a patch), 0 when the caller must
+// patch them: no ids, a second release of the same seq (commit_wait released
+// it already, with mode 0), or a kernel that gave up waiting before the
+// release came (its acknowledgement says it did not patch).
 extern "C" int airs_dev_commit_release(struct airs_dev_engine *e, uint32_t seq, const uint64_t *ids, uint32_t total)
 {
+	if (e->hco_released == seq)
+		return 0;
+	e->hco_released = seq;
 	if (ids && total > AIRS_HCO_MAX_IDS)
 		ids = nullptr;
 	if (ids)
@@ -2218,7 +2265,21 @@ extern "C" int airs_dev_commit_release(struct airs_dev_engine *e, uint32_t seq, 
 	e->hco[AIRS_HCO_MODE] = ids ? 1u : 0u;
 	__atomic_thread_fence(__ATOMIC_SEQ_CST);
 	e->hco[AIRS_HCO_GO] = seq;
-	return ids ? 1 : 0;
+	if (!ids)
+		return 0;
+	// the kernel signalled (commit_wait) and is waiting or has given up: its
+	// acknowledgement follows within its patch time
+	const uint32_t want = (seq & 0x7FFFFFFFu) << 1;
+	for (uint64_t i = 0; i < e->commit_polls + 1024u; i++) {
+		const uint32_t ack = e->hco[AIRS_HCO_ACK];
+		if ((ack & ~1u) == want)
+			return (int)(ack & 1u);
+		__builtin_ia32_pause();
+	}
+	if (sync_wait(e, false)) // the kernel has ended (or the stream faulted)
+		return 0;
+	const uint32_t ack = e->hco[AIRS_HCO_ACK];
+	return (ack & ~1u) == want ? (int)(ack & 1u) : 0;
 }
 
 static uint32_t sync_wait(struct airs_dev_engine *e, bool waited)

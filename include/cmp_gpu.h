@@ -89,7 +89,12 @@ void cmp_gpu_engine_destroy(struct cmp_gpu_engine *engine);
  *                               index when its whole grid fits the CUs; without
  *                               it every workgroup numbers itself with a
  *                               ticket as it starts, which stays correct beside
- *                               other kernels and processes.
+ *                               other kernels and processes.  CMP_GPU_AUTO_RICE
+ *                               picks k inside the encode kernel for frames of
+ *                               up to 32 segments (16-bit: 512 Ki samples) with
+ *                               the option, up to 8 without it (a frame's
+ *                               segments meet at a barrier); larger frames take
+ *                               the selection kernel first.
  *   CMP_GPU_OPT_WALK_SEGMENT    MODEL segment walk: 0 automatic, or 2048 /
  *                               4096 samples per segment.
  *   CMP_GPU_OPT_NO_CONTEXT_WALK 1: MODEL batches take the segment walk where

@@ -139,6 +139,64 @@ def test_autorice_vs_oracle(prod, eng, orc, orc_ext, kind, pre, n):
                      f"{[(api.parse_header(got[f])['encoder_param'], api.parse_header(want[f])['encoder_param']) for f in bad[:4]]}")
 
 
+@pytest.fixture(scope="module")
+def eng_x(prod):
+    """an engine marked CMP_GPU_OPT_EXCLUSIVE: frames of 9 .. AUTO_MAX_SPF
+    segments choose k inside the encode kernel (without the option they take
+    the selection kernel first)"""
+    if not prod.gpu_available():
+        pytest.fail("GPU test run without a usable HIP device")
+    e = prod.engine()
+    assert e.set_option(load_pkg().OPT_EXCLUSIVE, 1) == 0
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("kind,pre,n", [("u16", 1, 9 * SEG16), ("i16", 0, 17 * SEG16 + 3), ("u16", 0, AUTO_MAX_SPF * SEG16),
+                                        ("i16_in_i32", 1, AUTO_MAX_SPF * SEG32), ("u16", 1, AUTO_MAX_SPF * SEG16 + 1)])
+def test_autorice_exclusive_engine_vs_oracle(prod, eng_x, orc, orc_ext, kind, pre, n):
+    rng = np.random.default_rng(zlib.crc32(f"x/{kind}/{pre}/{n}".encode()))
+    frames = _frames(rng, kind, n, 6, extreme=True)
+    want = _oracle(orc, orc_ext, kind, pre, frames)
+    got = _gpu(prod, eng_x, kind, pre, frames)
+    bad = [f for f in range(len(frames)) if _mask(got[f]) != _mask(want[f])]
+    assert not bad, f"frames {bad[:8]} differ"
+
+
+def test_autorice_beside_other_kernels(prod, eng, orc, orc_ext):
+    """a cfg3-shaped AUTO batch (frames of 64 Ki u16, 4
+    segments, DIFF; the fused selection, whose segments meet at their frame's
+    candidate barrier) on an engine NOT marked exclusive, while kernels on a
+    second stream keep the CUs busy: bit-exact, and no look-back or barrier
+    give-up (CMP_ERR_INT_BITSTREAM from cmp_gpu_synchronize, which _gpu
+    checks)."""
+    import threading
+
+    import torch
+    rng = np.random.default_rng(7)
+    frames = _frames(rng, "u16", 4 * SEG16, 96, extreme=False)
+    want = _oracle(orc, orc_ext, "u16", 1, frames)
+    side = torch.cuda.Stream()
+    buf = torch.empty(1 << 27, dtype=torch.float32, device="cuda")  # 512 MiB of elementwise work per op
+    stop = threading.Event()
+
+    def load():
+        with torch.cuda.stream(side):
+            while not stop.is_set():
+                buf.mul_(1.0001).add_(0.5)
+                side.synchronize()
+    t = threading.Thread(target=load)
+    t.start()
+    try:
+        got = [_gpu(prod, eng, "u16", 1, frames) for _ in range(3)]
+    finally:
+        stop.set()
+        t.join()
+    for g in got:
+        bad = [f for f in range(len(frames)) if _mask(g[f]) != _mask(want[f])]
+        assert not bad, f"frames {bad[:8]} differ"
+
+
 def test_autorice_k_range(prod, eng, orc, orc_ext):
     """The sweep reaches every k: scales 2^-1 .. 2^15.5 over 64 frames."""
     rng = np.random.default_rng(11)

@@ -261,6 +261,50 @@ def test_batch_segment_walk_fallback(prod, eng, orc, kind, n, nctx, p_noise, sep
     assert not bad, f"frames {bad[:8]} differ"
 
 
+@pytest.mark.parametrize("knob", ["AIRS_TEST_COMMIT_TICKS", "AIRS_TEST_COMMIT_POLLS"])
+def test_batch_commit_give_up_paths(prod, orc, knob):
+    """the speculative segment walk's commit handshake when
+    one side gives up waiting.  AIRS_TEST_COMMIT_TICKS=0: the commit kernel
+    stops waiting for the host's release at once (as if the host thread had
+    been descheduled for a second); AIRS_TEST_COMMIT_POLLS=0: the host stops
+    waiting for the kernel's signal at once (as if earlier work still held the
+    stream) and releases without identifiers.  Either way the headers must
+    still carry the identifiers (the host patches them when the kernel's
+    acknowledgement says it did not): frames with identifiers unmasked,
+    sizes and context states against the oracle's call loop."""
+    import os
+
+    import numpy as np
+    import torch
+    P = api.CmpParams
+    params = P(primary_preprocessing=1, primary_encoder_type=1, primary_encoder_param=16,
+               secondary_iterations=15, secondary_preprocessing=3, secondary_encoder_type=2,
+               secondary_encoder_param=8, secondary_encoder_outlier=107, model_rate=11,
+               checksum_enabled=1, uncompressed_fallback_enabled=1)
+    rng = np.random.default_rng(404)
+    n, nctx, fpc = 16384, 8, 5
+    srcs = []
+    for c in range(nctx):
+        base = np.cumsum(rng.integers(-3, 4, n))
+        for a in range(fpc):
+            v = (base + rng.integers(-4, 5, n)).astype(np.int64)  # nothing falls back: the kernel patches
+            srcs.append((v & 0xFFFF).astype(np.uint16))
+    cap = 26 + 6 * n
+    want = bs.run_batch_host(orc, api, params, "u16", n, nctx, fpc, cap, srcs, splits=[2, 3])
+    os.environ[knob] = "0"
+    try:
+        e = prod.engine(torch.cuda.current_stream().cuda_stream)  # reads the knob at creation
+    finally:
+        del os.environ[knob]
+    try:
+        got = bs.run_batch_gpu(prod, e, api, params, "u16", n, nctx, fpc, cap, srcs, splits=[2, 3])
+    finally:
+        e.close()
+    assert got[1] == want[1], "context states or work buffers differ"
+    bad = [f for f in range(nctx * fpc) if got[0][f] != want[0][f]]
+    assert not bad, f"frames {bad[:8]} differ"
+
+
 def test_batch_mixed_fallback_model_contexts(prod, eng, orc):
     """contexts with and without the uncompressed fallback
     in one batch (different parameters: the host-stepped path), with
