@@ -541,6 +541,7 @@ size_t walk_seg_lds(uint32_t img_words, uint32_t fpc);
 // the Rice/ZERO frame kernel (enc_rice.hip): 16-bit NONE/DIFF, one g = 2^k
 // (k <= 7), no model, whole 16 Ki-sample segments; false: not eligible
 bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s, bool stream);
+bool rice_auto_encode(const KArgs &k, uint32_t pre, hipStream_t s);
 void stream_encode(const KArgs &k, uint32_t sample_bytes, uint32_t pre, uint32_t enc, bool rice, bool full,
 		   uint32_t grid, hipStream_t s);
 

@@ -429,6 +429,178 @@ __device__ __forceinline__ void rice_store(const uint32_t *Lx, uint32_t Pc, uint
 	}
 }
 
+// AUTO: the predecessor's last 32 bits (its tail granule, published once it
+// knows the frame's k), polled by wave 0 (bounded as every wait)
+__device__ __forceinline__ uint32_t rice_tail_wait(const KArgs &a, uint32_t gseg)
+{
+	uint64_t tv = gran_load(&a.tail[gseg - 1u]);
+	for (uint32_t s2 = 0; (uint32_t)(tv >> 32) != a.epoch; s2++) {
+		if (s2 > AIRS_SPIN_LIMIT) {
+			if ((threadIdx.x & 63u) == 0)
+				atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+			break;
+		}
+		__builtin_amdgcn_s_sleep(1);
+		tv = gran_load(&a.tail[gseg - 1u]);
+	}
+	return (uint32_t)tv;
+}
+
+// AUTO (CMP_GPU_AUTO_RICE, fused): the frame's k and this segment's payload
+// bit offset (header excluded), from the mapped pairs mp, as encode_kernel's
+// AUTO (enc_kernel.h): a 129-bin histogram of v = m + 1 in
+// the (zeroed) arena, one 32-bit counter per (bin, lane) shared by the four
+// waves (bank = lane); the bin totals; the segment's 16 candidate sums
+// S_k = sum min(v >> k, 16), published as epoch-tagged granules; wave 0
+// reads the frame's spf * 16 granules (the frame barrier), takes the k with
+// the fewest bits n (k + 1) + S_k (ties to the smaller k) and the sum of
+// S_k over the segments before this one.  Leaves the arena zero again.
+__device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const uint32_t (&mp)[RCH][8], uint32_t gseg, uint32_t sif,
+			     uint32_t tid, uint32_t lane, uint32_t wid)
+{
+	__shared__ uint32_t s_hist[AUTO_BINS];
+	__shared__ uint32_t s_kt[RNW][16];
+	__shared__ uint32_t s_res[2];
+	// this lane's counter of bin b is at byte hbase + 256 (b + 1016): the bin's
+	// offset comes from the float bits with one shift and one shift-add (the
+	// 32-bit LDS address arithmetic wraps)
+	const uint32_t hbase = (uint32_t)(uintptr_t)H + 4u * lane - 1016u * 256u;
+	__syncthreads(); // the arena is zeroed
+#pragma unroll
+	for (uint32_t c = 0; c < RCH; c++) {
+#pragma unroll
+		for (uint32_t jp = 0; jp < 8u; jp++) {
+			// an opaque copy of the pair: otherwise the compiler computes all
+			// 64 bins ahead of the barrier above
+			uint32_t wv = mp[c][jp];
+			asm volatile("" : "+v"(wv));
+#pragma unroll
+			for (uint32_t h = 0; h < 2; h++) {
+				const uint32_t v = (h ? wv >> 16 : wv & 0xFFFFu) + 1u;
+				uint32_t ha;
+				asm("v_lshrrev_b32 %0, 20, %1\n\tv_lshl_add_u32 %0, %0, 8, %2"
+				    : "=&v"(ha)
+				    : "v"(__float_as_uint((float)v)), "v"(hbase));
+				__hip_atomic_fetch_add(reinterpret_cast<lds_u32 *>((uintptr_t)ha), 1u, __ATOMIC_RELAXED,
+						       __HIP_MEMORY_SCOPE_WORKGROUP);
+			}
+		}
+	}
+	__syncthreads();
+	// bin totals: threads 2r, 2r + 1 sum the halves of row r < 128 with eight
+	// 16-byte reads each, rotated by r (4-way bank sharing); wave 0 row 128
+	{
+		const uint32_t r = tid >> 1, h = tid & 1u;
+		const uint4 *row = reinterpret_cast<const uint4 *>(H + r * 64u + h * 32u);
+		uint32_t sm = 0u;
+#pragma unroll
+		for (uint32_t hq = 0; hq < 8u; hq += 4u) {
+			uint4 q4[4];
+#pragma unroll
+			for (uint32_t q = 0; q < 4u; q++)
+				q4[q] = row[(hq + q + r) & 7u];
+#pragma unroll
+			for (uint32_t q = 0; q < 4u; q++)
+				sm += q4[q].x + q4[q].y + q4[q].z + q4[q].w;
+		}
+		sm += __shfl_xor(sm, 1, 64);
+		if (h == 0u)
+			s_hist[r] = sm;
+		static_assert(AUTO_BINS == RWG / 2u + 1u, "rows 0..127 by thread pairs, then row 128");
+		if (wid == 0) {
+			const uint32_t s128 = wave_sum(H[128u * 64u + lane]);
+			if (lane == 0)
+				s_hist[128] = s128;
+		}
+	}
+	__syncthreads();
+	// the arena again as the arena: clear the histogram rows
+	for (uint32_t i = tid; i < AUTO_BINS * 64u / 4u; i += RWG)
+		reinterpret_cast<uint4 *>(H)[i] = make_uint4(0u, 0u, 0u, 0u);
+	// the segment's 16 candidate sums: thread (slice sl, k) covers bins sl,
+	// sl + 16, ...; the four slices of a wave meet through two shuffles
+	{
+		const uint32_t k = tid & 15u, sl = tid >> 4;
+		uint32_t part = 0u;
+#pragma unroll
+		for (uint32_t i = 0; i < (AUTO_BINS + 15u) / 16u; i++) {
+			const uint32_t b = sl + 16u * i;
+			if (b < AUTO_BINS)
+				part += s_hist[b] * auto_term(b, k);
+		}
+		part += __shfl_xor(part, 16, 64);
+		part += __shfl_xor(part, 32, 64);
+		if (lane < 16u)
+			s_kt[wid][k] = part;
+	}
+	__syncthreads();
+	if (wid == 0) {
+		// publish (lanes 0-15), then read the frame's 16 * spf granules
+		if (lane < 16u) {
+			uint32_t sk = 0u;
+#pragma unroll
+			for (uint32_t w = 0; w < RNW; w++)
+				sk += s_kt[w][lane];
+			gran_store(&a.ktot[(uint64_t)gseg * 16u + lane], ((uint64_t)a.epoch << 32) | sk);
+		}
+		const uint32_t first_seg = gseg - sif, ng = a.segs_per_frame * 16u;
+		constexpr uint32_t NL = (AUTO_MAX_SPF + 3u) / 4u; // granule loads per lane
+		uint64_t gk[NL];
+#pragma unroll
+		for (uint32_t i = 0; i < NL; i++) {
+			const uint32_t gi = 64u * i + lane;
+			gk[i] = gi < ng ? gran_load(&a.ktot[(uint64_t)first_seg * 16u + gi]) : 0ull;
+		}
+		for (uint32_t spins = 0;;) {
+			bool bad = false;
+#pragma unroll
+			for (uint32_t i = 0; i < NL; i++)
+				bad |= 64u * i + lane < ng && (uint32_t)(gk[i] >> 32) != a.epoch;
+			if (!__ballot(bad))
+				break;
+			if (++spins > AIRS_SPIN_LIMIT) {
+				if (lane == 0)
+					atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+				break;
+			}
+			__builtin_amdgcn_s_sleep(1);
+#pragma unroll
+			for (uint32_t i = 0; i < NL; i++) {
+				const uint32_t gi = 64u * i + lane;
+				if (gi < ng && (uint32_t)(gk[i] >> 32) != a.epoch)
+					gk[i] = gran_load(&a.ktot[(uint64_t)first_seg * 16u + gi]);
+			}
+		}
+		// lane l holds segment 4 i + l / 16, candidate k = l % 16
+		uint32_t tot = 0u, pre = 0u;
+#pragma unroll
+		for (uint32_t i = 0; i < NL; i++) {
+			const uint32_t gi = 64u * i + lane;
+			const uint32_t v = gi < ng ? (uint32_t)gk[i] : 0u;
+			tot += v;
+			pre += (gi >> 4) < sif ? v : 0u;
+		}
+		tot += __shfl_xor(tot, 16, 64);
+		tot += __shfl_xor(tot, 32, 64);
+		pre += __shfl_xor(pre, 16, 64);
+		pre += __shfl_xor(pre, 32, 64);
+		const uint32_t k = lane & 15u;
+		// frame bits for k (< 2^28: spf <= 32 segments), ties to the smaller k
+		uint32_t key = ((tot + a.n * (k + 1u)) << 4) | k;
+#pragma unroll
+		for (uint32_t dd = 1; dd < 16u; dd <<= 1)
+			key = min(key, (uint32_t)__shfl_xor(key, dd, 64));
+		const uint32_t ks = key & 15u;
+		const uint32_t pre_k = __shfl(pre, ks, 64);
+		if (lane == 0) {
+			s_res[0] = ks;
+			s_res[1] = pre_k + sif * RSEGN * (ks + 1u); // every segment before this one is whole
+		}
+	}
+	__syncthreads();
+	return make_uint2(__builtin_amdgcn_readfirstlane(s_res[0]), __builtin_amdgcn_readfirstlane(s_res[1]));
+}
+
 // the lane's samples of segment `sif` of a frame: 4 chunks x 16 samples, and
 // for DIFF the sample before each chunk's first (lane 0 of each wave uses it;
 // every lane loads, so the load needs no branch; 0 before the frame's first
@@ -464,9 +636,10 @@ __device__ __forceinline__ void rice_load(const KArgs &a, const uint8_t *fsrc, u
 	}
 }
 
-template <int PRE, bool STREAM>
+template <int PRE, bool STREAM, bool AUTO = false>
 __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_WPE, 8))) void rice_kernel(KArgs a)
 {
+	static_assert(!(AUTO && STREAM), "AUTO: frames only");
 	// 22-byte header (GOLOMB_ZERO); STREAM (cmp_gpu_encode_stream): one frame,
 	// payload only (no header, checksum or 24-bit size field)
 	constexpr uint32_t HDR_BITS = STREAM ? 0u : 176u;
@@ -480,9 +653,23 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 	const uint32_t nfr = a.num_segs / a.segs_per_frame;
 	// Frame-interleaved order (as encode_kernel): dispatch index d is segment
 	// d / nfr of launch frame d % nfr, so a frame's segments come in order.
-	// One segment per workgroup, d = the block index.
+	// One segment per workgroup, d = the block index.  AUTO: frame-major and
+	// XCD-local instead (as encode_kernel's AUTO): frame 8 j + x takes blocks
+	// x + 8 (j spf + s), so that a frame's segments, which meet at the
+	// candidate barrier, are dispatched together on one XCD; the grid is padded
+	// to whole groups of 8 frames.
 	const uint32_t d = blockIdx.x;
-	const uint32_t sif = d / nfr, lf = d - sif * nfr;
+	uint32_t sif, lf;
+	if constexpr (AUTO) {
+		const uint32_t p = d >> 3;
+		sif = p % a.segs_per_frame;
+		lf = 8u * (p / a.segs_per_frame) + (d & 7u);
+		if (lf >= nfr)
+			return; // padding block
+	} else {
+		sif = d / nfr;
+		lf = d - sif * nfr;
+	}
 	const uint32_t gseg = lf * a.segs_per_frame + sif;
 	const uint32_t frame =
 		__builtin_amdgcn_readfirstlane(a.frame_list ? a.frame_list[lf] : a.frame_add + lf * a.frame_mul);
@@ -500,13 +687,46 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		for (uint32_t i = tid; i < a.img_words / 4u; i += RWG)
 			L4[i] = make_uint4(0u, 0u, 0u, 0u);
 	}
-	const Coder cd = make_coder<ENC_ZERO>(__builtin_amdgcn_readfirstlane(a.g), a.outlier_param);
-	const uint32_t k = cd.k;
-	if (tid < 18u)
-		s_tab[tid] = rice_table_entry(tid, k);
-	__syncthreads(); // B0: table and zeroed arena
-
 	const bool is_first = sif == 0u, is_last = sif + 1u == a.segs_per_frame;
+	Coder cd;
+	uint32_t k, auto_P = 0u;
+	uint32_t mp[AUTO ? RCH : 1][8]; // AUTO: the mapped pairs, kept across the frame's k choice
+	if constexpr (AUTO) {
+		// ---- AUTO: residuals, histogram, the frame's k -----
+#pragma unroll
+		for (uint32_t c = 0; c < RCH; c++) {
+			const uint32_t w[8] = {raw[c][0].x, raw[c][0].y, raw[c][0].z, raw[c][0].w,
+					       raw[c][1].x, raw[c][1].y, raw[c][1].z, raw[c][1].w};
+			const uint32_t pv0 = (c == 0u && sif == 0u && wid == 0u) ? 0u : prevld[c];
+			const uint32_t wprev = PRE == PRE_DIFF ? (uint32_t)__builtin_amdgcn_update_dpp(
+									 (int)(pv0 << 16), (int)w[7], 0x138, 0xF, 0xF, false)
+							       : 0u;
+#pragma unroll
+			for (uint32_t j = 0; j < 8u; j++) {
+				uint32_t u = w[j];
+				if (PRE == PRE_DIFF)
+					u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
+				mp[AUTO ? c : 0][j] = zigzag_pk(u);
+			}
+#pragma unroll
+			for (uint32_t j = 0; j < 8u; j++)
+				asm volatile("" : "+v"(mp[AUTO ? c : 0][j]));
+		}
+		const uint2 ks = rice_auto_k(a, L_ar, mp, gseg, sif, tid, lane, wid);
+		k = ks.x;
+		auto_P = ks.y + HDR_BITS;
+		cd = make_coder<ENC_ZERO>(1u << k, a.outlier_param);
+		if (tid < 18u)
+			s_tab[tid] = rice_table_entry(tid, k);
+		__syncthreads(); // the table; the arena is zero again (rice_auto_k)
+	} else {
+		cd = make_coder<ENC_ZERO>(__builtin_amdgcn_readfirstlane(a.g), a.outlier_param);
+		k = cd.k;
+		if (tid < 18u)
+			s_tab[tid] = rice_table_entry(tid, k);
+		__syncthreads(); // B0: table and zeroed arena
+	}
+
 	// ---- phase 1: codeword pairs and lengths -----------------------------
 	// V[c][j]: the codewords of samples 2j, 2j+1 of the lane's chunk c back to
 	// back (or the two mapped values when they exceed 32 bits); lp[c]: the
@@ -521,15 +741,19 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		// the pair ending with the sample before the lane's first: lane i - 1's
 		// last pair (DPP wave_shr:1), lane 0 the loaded sample
 		const uint32_t pv0 = (c == 0u && sif == 0u && wid == 0u) ? 0u : prevld[c]; // 0 before the frame's first sample
-		const uint32_t wprev = PRE == PRE_DIFF ? (uint32_t)__builtin_amdgcn_update_dpp(
-								 (int)(pv0 << 16), (int)w[7], 0x138, 0xF, 0xF, false)
-						       : 0u;
+		const uint32_t wprev = !AUTO && PRE == PRE_DIFF ? (uint32_t)__builtin_amdgcn_update_dpp(
+									  (int)(pv0 << 16), (int)w[7], 0x138, 0xF, 0xF, false)
+								: 0u;
 #pragma unroll
 		for (uint32_t j = 0; j < 8u; j++) {
-			uint32_t u = w[j];
-			if (PRE == PRE_DIFF)
-				u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
-			m[j] = zigzag_pk(u);
+			if constexpr (AUTO) {
+				m[j] = mp[AUTO ? c : 0][j];
+			} else {
+				uint32_t u = w[j];
+				if (PRE == PRE_DIFF)
+					u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
+				m[j] = zigzag_pk(u);
+			}
 			const u16x2 v = __builtin_elementwise_add_sat(pk(m[j]), (u16x2)(1));
 			q8[j] = unpk(__builtin_elementwise_min(v >> (u16x2)((unsigned short)k), (u16x2)(17)) << (u16x2)(3));
 		}
@@ -647,7 +871,7 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 			A += tot[c];
 		}
 	}
-	if (wid == 0 && lane == 0) {
+	if (!AUTO && wid == 0 && lane == 0) { // (AUTO: the offset is known from the candidates)
 		const uint64_t tag = ((uint64_t)a.epoch << 1) | (is_first ? 1u : 0u);
 		gran_store(&a.agg[gseg], (tag << 32) | (is_first ? HDR_BITS + A : A));
 	}
@@ -674,11 +898,13 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 				dbg_stamp(a, gseg, 3);
 				if (DBG(2u)) // ablation: no look-back (offsets invented, output garbage)
 					pp = make_uint2(HDR_BITS + sif * 37u, 0u);
+				else if (AUTO)
+					pp = make_uint2(auto_P, is_first ? hdr_pred : rice_tail_wait(a, gseg));
 				else if (!is_first)
 					pp = (a.lbmode & 1u) && sif >= 16u ? rice_lookback_s(a, gseg, sif, lane)
 									     : rice_lookback(a, gseg, sif, lane, 0ull);
 				if (lane == 0) {
-					if (!is_first)
+					if (!AUTO && !is_first)
 						gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (pp.x + A));
 					s_misc[0] = pp.x;
 					s_misc[1] = pp.y;
@@ -705,11 +931,13 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 		// through the arena (every chunk fits: 4096 x (k + 17) bits) --------
 		if (wid == 0) {
 			uint2 pp = make_uint2(HDR_BITS, hdr_pred);
-			if (!is_first)
+			if (AUTO)
+				pp = make_uint2(auto_P, is_first ? hdr_pred : rice_tail_wait(a, gseg));
+			else if (!is_first)
 				pp = (a.lbmode & 1u) && sif >= 16u ? rice_lookback_s(a, gseg, sif, lane)
 								     : rice_lookback(a, gseg, sif, lane, 0ull);
 			if (lane == 0) {
-				if (!is_first)
+				if (!AUTO && !is_first)
 					gran_store(&a.agg[gseg], ((((uint64_t)a.epoch << 1) | 1u) << 32) | (pp.x + A));
 				s_misc[0] = pp.x;
 				s_misc[1] = pp.y;
@@ -826,6 +1054,33 @@ bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s, bool stream)
 	else
 		kern = pre == PRE_DIFF ? rice_kernel<PRE_DIFF, false> : rice_kernel<PRE_NONE, false>;
 	hipLaunchKernelGGL(kern, dim3(ka.num_segs), dim3(RWG), lds, s, ka);
+	return true;
+}
+
+// CMP_GPU_AUTO_RICE with the k chosen in the kernel (frames of at most
+// AUTO_MAX_SPF segments, no model): the Rice kernel with the candidate
+// barrier in place of the look-back; false when the launch does not fit it
+// (16-bit NONE/DIFF, whole 16 Ki-sample segments, 16-byte aligned frames),
+// the caller then takes encode_kernel's AUTO.
+bool rice_auto_encode(const KArgs &k, uint32_t pre, hipStream_t s)
+{
+	if (pre != PRE_NONE && pre != PRE_DIFF)
+		return false;
+	if (!k.ktot || k.frame_g || k.model_mode || k.segs_per_frame == 0u || k.n % RSEGN)
+		return false;
+	const uint32_t nfr = k.num_segs / k.segs_per_frame;
+	KArgs ka = k;
+	ka.segs_per_frame = k.n / RSEGN;
+	if (ka.segs_per_frame != k.segs_per_frame || ka.segs_per_frame > AUTO_MAX_SPF)
+		return false; // (the candidate granules are laid out per caller segment)
+	ka.num_segs = nfr * ka.segs_per_frame;
+	ka.img_words = rice_arena_words();
+	const uint32_t grid = (nfr + 7u) / 8u * 8u * ka.segs_per_frame;
+	const size_t lds = (size_t)ka.img_words * 4u;
+	if (pre == PRE_DIFF)
+		hipLaunchKernelGGL((rice_kernel<PRE_DIFF, false, true>), dim3(grid), dim3(RWG), lds, s, ka);
+	else
+		hipLaunchKernelGGL((rice_kernel<PRE_NONE, false, true>), dim3(grid), dim3(RWG), lds, s, ka);
 	return true;
 }
 

@@ -1408,6 +1408,12 @@ static void launch_encode(const KArgs &k, bool full, uint32_t grid, hipStream_t 
 {
 	if constexpr (ENC == ENC_ZERO && RICE && MODEL == 0 && (PRE == PRE_NONE || PRE == PRE_DIFF)) {
 		if (k.ktot) { // fused per-frame Rice selection (frame barrier: never persistent)
+#ifndef AIRS_RICE_AUTO
+#define AIRS_RICE_AUTO 1
+#endif
+			// the Rice kernel with the candidate barrier (enc_rice.hip)
+			if (AIRS_RICE_AUTO && W == 2 && full && rice_auto_encode(k, PRE, s))
+				return;
 			size_t lds = (size_t)2u * (k.img_words + 4u) * 4u; // two images (enc_kernel.h NIMG)
 			lds = lds > AUTO_BINS * 64u * 4u ? lds : AUTO_BINS * 64u * 4u; // the histogram
 			if (full)

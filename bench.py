@@ -596,8 +596,9 @@ def main():
         "cfg2": rice + ": one launch per step",
         "cfg2s": ("airs::rice_kernel<DIFF,STREAM> (enc_rice.hip: 16 Ki-sample segments, no header): one launch "
                   "per step, one look-back chain of 4096 segments"),
-        "cfg3": ("airs::encode_kernel<2,DIFF,ZERO,Rice,0,FULL,AUTO> (the per-frame Rice k chosen in-kernel from a "
-                 "histogram of the samples in registers): one launch per step"),
+        "cfg3": ("airs::rice_kernel<DIFF,AUTO> (enc_rice.hip: the per-frame Rice k chosen in-kernel from a "
+                 "histogram of the samples in registers, the frame's segments meeting at a candidate barrier "
+                 "instead of a look-back; then the Rice kernel's codeword pairs and arena): one launch per step"),
         "cfg4": rice + ": one launch per step",
         "cfg5": "airs::walk_ctx_kernel<4,DIFF,ZERO,Rice,MULTI,Rice,4> (enc_walk.hip): ONE launch per step, one "
                 "1024-thread workgroup per stream walks its 16 acquisitions, the model in registers",

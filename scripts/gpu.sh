@@ -12,6 +12,7 @@
 #   kbt:W[:LIB]      kb:W under a rocprofv3 kernel trace (110 launches, per-launch durations)
 #   ts:W:LIB         the per-segment timeline ring of 110 cold launches (ablation build LIB,
 #                    AIRS_DBG 65536, or $AIRS_DBG) under a kernel trace; scripts/ts_launches.py reads it
+#   run:NAME         exp/bin/NAME (a micro-benchmark built from scripts/NAME.hip)
 #   env:VAR=VALUE    export VAR for the following steps;  unset:VAR  drop it again
 # kb, kbt and ts take an optional 4th field, a tag appended to their output names.
 # Environment variables set before the command (AIRS_*) reach every step.
@@ -21,8 +22,7 @@ O=gpurun_out/$TAG
 cd "$GRAFT_REPO_ROOT" && mkdir -p $O && export TMPDIR=/tmp || exit 1
 kern() {
 	case $1 in
-	cfg2 | cfg2s | cfg4) echo rice_kernel ;;
-	cfg3) echo encode_kernel ;;
+	cfg2 | cfg2s | cfg3 | cfg4) echo rice_kernel ;;
 	cfg5 | cfg5fb) echo walk_ctx_kernel ;;
 	cfg5s8 | cfg5fbs8) echo walk_kernel ;;
 	esac
@@ -94,6 +94,11 @@ for st in "$@"; do
 		[ "$w" = cfg4 ] && spf=4
 		python3 scripts/ts_launches.py $d.bin $((110 + ${AIRS_KB_PRE:-0})) $spf >$d.txt 2>&1
 		gzip $d.bin
+		;;
+	run)
+		# run:NAME  a prebuilt exp/bin/NAME (scripts/*.hip micro-benchmarks)
+		timeout -k 10 120 exp/bin/$w >$O/run_$w.txt 2>&1 || { tail -5 $O/run_$w.txt; exit 1; }
+		cat $O/run_$w.txt
 		;;
 	env)
 		export "$w${x:+:$x}"

@@ -24,9 +24,13 @@ BUDGETS = {
     # (round 6: the scalar look-back of XCD-local frames, rice_lookback_s,
     # holds a 16-granule window in 32 SGPRs: 19 spills to VGPR lanes, all in
     # wave 0's look-back, once per segment)
-    "_ZN4airs11rice_kernelILi1ELb0EEEvNS_5KArgsE": (96, 24),
-    "_ZN4airs11rice_kernelILi0ELb0EEEvNS_5KArgsE": (96, 24),
-    "_ZN4airs11rice_kernelILi1ELb1EEEvNS_5KArgsE": (96, 0),
+    "_ZN4airs11rice_kernelILi1ELb0ELb0EEEvNS_5KArgsE": (96, 24),
+    "_ZN4airs11rice_kernelILi0ELb0ELb0EEEvNS_5KArgsE": (96, 24),
+    "_ZN4airs11rice_kernelILi1ELb1ELb0EEEvNS_5KArgsE": (96, 0),
+    # cfg3: the Rice kernel with the frame's k chosen in it (AUTO; round 6):
+    # the 64 mapped samples stay in registers across the candidate barrier
+    "_ZN4airs11rice_kernelILi1ELb0ELb1EEEvNS_5KArgsE": (112, 0),
+    "_ZN4airs11rice_kernelILi0ELb0ELb1EEEvNS_5KArgsE": (112, 0),
     # encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>: frames the Rice
     # kernel does not take (k > 7, holes in device-planned launch lists); no
     # longer a bench path, so the kernel-argument padding that kept it at 13
