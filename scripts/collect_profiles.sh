@@ -1,8 +1,8 @@
 # Copy a round's GPU evidence from gpurun_out/ into profiles/ (tracked):
 #   collect_profiles.sh RUN_TAG PROF_TAG PMC_TAG PREFIX
-# RUN_TAG: gpu_r05_round.sh without profiles (tests, smoke, bench lines);
-# PROF_TAG: the same with SKIP_TESTS/SKIP_BENCH (kernel stats, FETCH/WRITE traffic);
-# PMC_TAG: gpu_pmc.sh (pmc_summary.json).  Missing pieces are skipped.
+# RUN_TAG: a scripts/gpu.sh run with tests and bench:W steps;
+# PROF_TAG: one with kt:W and traffic:W steps (kernel stats, FETCH/WRITE traffic);
+# PMC_TAG: one with pmc:W:... steps (scripts/pmc_summary.py -> pmc_summary.json).  Missing pieces are skipped.
 R=gpurun_out/$1; P=gpurun_out/$2; M=gpurun_out/$3; X=profiles/$4
 for f in $R/bench_*.json; do [ -f "$f" ] && cp "$f" ${X}_$(basename "$f"); done
 [ -f $R/pytest_gpu.log ] && tail -5 $R/pytest_gpu.log > ${X}_pytest_gpu.txt
