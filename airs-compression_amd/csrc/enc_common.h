@@ -427,7 +427,9 @@ __device__ __forceinline__ uint2 rice_table_entry(uint32_t q, uint32_t k)
 {
 	if (q >= 17u)
 		return make_uint2(0u, k + 17u);
-	const uint32_t t = (1u << (q + k + 1u)) - (2u << k) - (q << k) + 1u;
+	// (64-bit: q + k + 1 reaches 32 for k = 15; the entry itself wraps mod
+	// 2^32, and cw = m + t stays exact since every codeword fits 32 bits)
+	const uint32_t t = (uint32_t)((1ull << (q + k + 1u)) - (2ull << k) - ((uint64_t)q << k) + 1ull);
 	return make_uint2(t, k + 1u + q);
 }
 

@@ -43,15 +43,31 @@ namespace airs {
 #ifndef AIRS_RICE_WG // threads per workgroup (256 or 512)
 #define AIRS_RICE_WG 256
 #endif
-#ifndef AIRS_RICE_WGPCU // workgroups per CU the LDS (and register allocation) is sized for
-#define AIRS_RICE_WGPCU 4
+// workgroups per CU the LDS arena (and the register allocation) is sized
+// for: DIFF frames 6 (round 6: with the scalar look-back the chains no
+// longer stall at more than four; cfg2 53.0-53.9 -> 50.1-53.5 us, with the
+// nt stores 47.8-51.2), NONE 5 (at 6 its registers spill to scratch), AUTO 4
+// (its mapped samples stay live across the candidate barrier: 99 VGPRs)
+#ifndef AIRS_RICE_WGPCU
+#define AIRS_RICE_WGPCU 6
 #endif
-#define AIRS_RICE_WPE (AIRS_RICE_WGPCU * AIRS_RICE_WG / 256) // waves per SIMD
+#ifndef AIRS_RICE_NONE_WGPCU
+#define AIRS_RICE_NONE_WGPCU 5
+#endif
+#ifndef AIRS_RICE_AUTO_WGPCU
+#define AIRS_RICE_AUTO_WGPCU 4
+#endif
 #ifndef AIRS_RICE_LBC // the look-back is evaluated after packing this many chunks (wave 0)
 #define AIRS_RICE_LBC 4
 #endif
 #ifndef AIRS_RICE_SLB // granules of the scalar first look-back round (16 or 32)
 #define AIRS_RICE_SLB 16
+#endif
+// cache policy of the payload stores (gfx950 aux: 2 = nt): the output is
+// written once and not read back by this kernel (round 6: a 128 MiB read +
+// 56 MiB dense write stream 34.3 -> 32.2 us, scripts/stream_bench.hip)
+#ifndef AIRS_RICE_STORE_AUX
+#define AIRS_RICE_STORE_AUX 2
 #endif
 #define RICE_KMAX 7u       // largest k this kernel takes (pairs of typical codes fit 32 bits)
 constexpr uint32_t RWG = AIRS_RICE_WG;      // threads per workgroup
@@ -64,10 +80,16 @@ constexpr uint32_t RGUARD = 4u;              // words before the arena (a lane's
 // and the rounding (measured: a 32464-byte workgroup admitted only four per CU)
 constexpr uint32_t RSTATIC = 2048u;
 
-// arena words (guard included) for AIRS_RICE_WPE workgroups per CU
-__host__ __device__ constexpr uint32_t rice_arena_words()
+template <int PRE, bool AUTO>
+__host__ __device__ constexpr uint32_t rice_wgpcu()
 {
-	return ((160u * 1024u / AIRS_RICE_WGPCU - RSTATIC) / 4u) & ~3u;
+	return AUTO ? AIRS_RICE_AUTO_WGPCU : PRE == PRE_NONE ? AIRS_RICE_NONE_WGPCU : AIRS_RICE_WGPCU;
+}
+
+// arena words (guard included) for `wgpcu` workgroups per CU
+__host__ __device__ constexpr uint32_t rice_arena_words(uint32_t wgpcu)
+{
+	return ((160u * 1024u / wgpcu - RSTATIC) / 4u) & ~3u;
 }
 
 // the four words of a lane's chunk: lengths of pairs 4h .. 4h+3, a byte each
@@ -409,14 +431,14 @@ __device__ __forceinline__ void rice_store(const uint32_t *Lx, uint32_t Pc, uint
 		o.y = bswap32(__builtin_amdgcn_alignbit(w.x, w.y, r));
 		o.z = bswap32(__builtin_amdgcn_alignbit(w.y, w.z, r));
 		o.w = bswap32(__builtin_amdgcn_alignbit(w.z, w.w, r));
-		__builtin_amdgcn_raw_buffer_store_b128(o, rsrc, (int)(4u * (g0 + j)), 0, 0);
+		__builtin_amdgcn_raw_buffer_store_b128(o, rsrc, (int)(4u * (g0 + j)), 0, AIRS_RICE_STORE_AUX);
 	}
 	const uint32_t rr = (tid - nquad) & (RWG - 1u);
 	if (rr < (nfull & 3u)) {
 		const uint32_t j = 4u * nquad + rr;
 		const uint32_t hi = j ? Ll[j - 1u] : predx;
 		__builtin_amdgcn_raw_buffer_store_b32(bswap32(__builtin_amdgcn_alignbit(hi, Ll[j], r)), rsrc,
-						      (int)(4u * (g0 + j)), 0, 0);
+						      (int)(4u * (g0 + j)), 0, AIRS_RICE_STORE_AUX);
 	}
 	if (finalx && nfull == J && tid == 0) {
 		const uint32_t hi = J ? Lx[J - 1u] : predx;
@@ -637,7 +659,8 @@ __device__ __forceinline__ void rice_load(const KArgs &a, const uint8_t *fsrc, u
 }
 
 template <int PRE, bool STREAM, bool AUTO = false>
-__global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_WPE, 8))) void rice_kernel(KArgs a)
+__global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(rice_wgpcu<PRE, AUTO>() * RWG / 256u, 8))) void
+rice_kernel(KArgs a)
 {
 	static_assert(!(AUTO && STREAM), "AUTO: frames only");
 	// 22-byte header (GOLOMB_ZERO); STREAM (cmp_gpu_encode_stream): one frame,
@@ -754,8 +777,20 @@ __global__ __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(AIRS_RICE_W
 					u = unpk(pk(w[j]) - pk(__builtin_amdgcn_alignbit(w[j], j ? w[j - 1] : wprev, 16)));
 				m[j] = zigzag_pk(u);
 			}
-			const u16x2 v = __builtin_elementwise_add_sat(pk(m[j]), (u16x2)(1));
-			q8[j] = unpk(__builtin_elementwise_min(v >> (u16x2)((unsigned short)k), (u16x2)(17)) << (u16x2)(3));
+			u16x2 q;
+			if (!AUTO || k <= 11u) {
+				// v = m + 1 saturates at 65535 for m = 65535: the same q after the
+				// clamp at 17 while 65535 >> k >= 17, i.e. k <= 11
+				const u16x2 v = __builtin_elementwise_add_sat(pk(m[j]), (u16x2)(1));
+				q = v >> (u16x2)((unsigned short)k);
+			} else {
+				// AUTO, k >= 12: (m + 1) >> k = (m >> k) + ((m & (2^k - 1)) + 1) >> k,
+				// every term below 2^16
+				const u16x2 mk = pk(m[j]);
+				const u16x2 lo = (mk & (u16x2)((unsigned short)((1u << k) - 1u))) + (u16x2)(1);
+				q = (mk >> (u16x2)((unsigned short)k)) + (lo >> (u16x2)((unsigned short)k));
+			}
+			q8[j] = unpk(__builtin_elementwise_min(q, (u16x2)(17)) << (u16x2)(3));
 		}
 		uint32_t t = 0u;
 #pragma unroll
@@ -1037,7 +1072,8 @@ bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s, bool stream)
 	const uint32_t nfr = k.num_segs / k.segs_per_frame;
 	ka.segs_per_frame = k.n / RSEGN;
 	ka.num_segs = nfr * ka.segs_per_frame;
-	ka.img_words = rice_arena_words();
+	ka.img_words = pre == PRE_DIFF ? rice_arena_words(rice_wgpcu<PRE_DIFF, false>())
+				       : rice_arena_words(rice_wgpcu<PRE_NONE, false>());
 	// block b runs on XCD b mod 8 (round-robin placement, MI355X_MICROARCH.md):
 	// with the frame-interleaved order, segment d and its predecessor d - nfr
 	// share an XCD when nfr is a multiple of 8 (speed only: every poll's
@@ -1074,7 +1110,8 @@ bool rice_auto_encode(const KArgs &k, uint32_t pre, hipStream_t s)
 	if (ka.segs_per_frame != k.segs_per_frame || ka.segs_per_frame > AUTO_MAX_SPF)
 		return false; // (the candidate granules are laid out per caller segment)
 	ka.num_segs = nfr * ka.segs_per_frame;
-	ka.img_words = rice_arena_words();
+	ka.img_words = pre == PRE_DIFF ? rice_arena_words(rice_wgpcu<PRE_DIFF, true>())
+				       : rice_arena_words(rice_wgpcu<PRE_NONE, true>());
 	const uint32_t grid = (nfr + 7u) / 8u * 8u * ka.segs_per_frame;
 	const size_t lds = (size_t)ka.img_words * 4u;
 	if (pre == PRE_DIFF)

@@ -56,6 +56,42 @@ __global__ __launch_bounds__(256) void seg32(const uint8_t *src, uint8_t *dst, u
 		sink[blockIdx.x] = x;
 }
 
+// writes: MODE 0 strided (segment i at dst + i * 32 KiB), 1 dense (dst + i *
+// WB: one contiguous compressed stream, as the encoder writes), 2 dense with
+// non-temporal stores; ONLYW: no reads at all
+template <int MODE, bool ONLYW>
+__global__ __launch_bounds__(256) void segw(const uint8_t *src, uint8_t *dst, uint32_t *sink)
+{
+	const uint32_t t = threadIdx.x;
+	uint32_t x = blockIdx.x;
+	if (!ONLYW) {
+		const uint8_t *s = src + (uint64_t)blockIdx.x * SEGB;
+		uint4 r[8];
+#pragma unroll
+		for (int c = 0; c < 4; c++) {
+			const uint4 *p = reinterpret_cast<const uint4 *>(s + c * 8192 + t * 32);
+			r[2 * c] = p[0];
+			r[2 * c + 1] = p[1];
+		}
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			x ^= r[i].x + r[i].y * 3u + r[i].z * 5u + r[i].w * 7u;
+	}
+	uint4 *d = reinterpret_cast<uint4 *>(dst + (uint64_t)blockIdx.x * (MODE == 0 ? SEGB : WB));
+	for (uint32_t i = t; i < WB / 16u; i += 256u) {
+		const uint4 v = make_uint4(x, x + i, x ^ i, i);
+		if (MODE == 2) {
+			typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+			u32x4 w = {v.x, v.y, v.z, v.w};
+			__builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(d + i));
+		} else {
+			d[i] = v;
+		}
+	}
+	if (x == 0x12345678u)
+		sink[blockIdx.x] = x;
+}
+
 template <bool W>
 __global__ __launch_bounds__(256) void coal(const uint8_t *src, uint8_t *dst, uint32_t *sink)
 {
@@ -139,6 +175,8 @@ int main()
 		{"seg32", seg32<false>, NSEG},   {"seg32_w", seg32<true>, NSEG}, {"coal", coal<false>, NSEG},
 		{"coal_w", coal<true>, NSEG},    {"pers1024", pers<false>, 1024}, {"pers1024_w", pers<true>, 1024},
 		{"pers2048", pers<false>, 2048}, {"pers2048_w", pers<true>, 2048}, {"pers512_w", pers<true>, 512},
+		{"w_strided", segw<0, false>, NSEG}, {"w_dense", segw<1, false>, NSEG}, {"w_dense_nt", segw<2, false>, NSEG},
+		{"wonly_dense", segw<1, true>, NSEG}, {"wonly_nt", segw<2, true>, NSEG},
 	};
 	hipEvent_t e0, e1;
 	CK(hipEventCreate(&e0));
