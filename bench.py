@@ -386,6 +386,25 @@ def timed_steps(torch, stream, step, bsets, steps, warmup, sync):
     return wall, ev0.elapsed_time(ev1) / steps
 
 
+def per_launch_us(torch, stream, step, bsets, n):
+    """The per-launch spread of the same cold steps (the mean of
+    the timed region hides a bimodal kernel): n more steps over the rotated
+    sets, each between its own HIP event pair on the engine stream.  Not
+    part of `value` (an event pair per step adds stream time of its own)."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    torch.cuda.synchronize()
+    for i, (e0, e1) in enumerate(evs):
+        e0.record(stream)
+        step(bsets[i % len(bsets)])
+        e1.record(stream)
+    torch.cuda.synchronize()
+    us = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in evs)
+    return dict(n=n, min=round(us[0], 2), p50=round(us[n // 2], 2), p90=round(us[(9 * n) // 10], 2),
+                max=round(us[-1], 2), max_over_min=round(us[-1] / us[0], 3),
+                note="each step of a separate cold pass after the timed region between its own HIP events "
+                     "(diagnostic: the spread of single launches, not part of value)")
+
+
 def make_sets(torch, pkg, lib, eng, wl, fids, rotate):
     """The buffer sets the timed steps rotate over: enough that one rotation
     touches more than the Infinity Cache (cold reads)."""
@@ -490,6 +509,9 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
+    launch_us = None
+    if world == 1:
+        launch_us = per_launch_us(torch, stream, step, sets, 20)
     warm = None
     if not args.no_warm and world == 1:
         wwall, wkern = timed(sets[:1], args.steps, 2)
@@ -663,6 +685,7 @@ def main():
                 "algorithmic_bytes_note": "compulsory HBM reads of one step: 2 B/sample (u16), 4 B/sample "
                                           "(i16-in-i32), +2 B/sample model read per MODEL pass (SURVEY 8(d))",
                 "avg_launch_ms_hip_events": round(kern_avg_ms, 5),
+                "launch_us": launch_us,
                 **({"frac_samples_only": round(in_bytes_rank / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "frac_samples_only_note": "the same launches against the sample bytes alone (4 B/sample): "
                                               "the model stays on the chip between acquisitions, so its 2 B/sample "
