@@ -760,7 +760,7 @@ rice_kernel(KArgs a)
 	for (uint32_t c = 0; c < RCH; c++) {
 		const uint32_t w[8] = {raw[c][0].x, raw[c][0].y, raw[c][0].z, raw[c][0].w,
 				       raw[c][1].x, raw[c][1].y, raw[c][1].z, raw[c][1].w};
-		uint32_t m[8], q8[8];
+		uint32_t m[8], q8[8]; // q8: min(q, 17) of both samples
 		// the pair ending with the sample before the lane's first: lane i - 1's
 		// last pair (DPP wave_shr:1), lane 0 the loaded sample
 		const uint32_t pv0 = (c == 0u && sif == 0u && wid == 0u) ? 0u : prevld[c]; // 0 before the frame's first sample
@@ -790,17 +790,23 @@ rice_kernel(KArgs a)
 				const u16x2 lo = (mk & (u16x2)((unsigned short)((1u << k) - 1u))) + (u16x2)(1);
 				q = (mk >> (u16x2)((unsigned short)k)) + (lo >> (u16x2)((unsigned short)k));
 			}
-			q8[j] = unpk(__builtin_elementwise_min(q, (u16x2)(17)) << (u16x2)(3));
+			q8[j] = unpk(__builtin_elementwise_min(q, (u16x2)(17)));
 		}
-		uint32_t t = 0u;
 #pragma unroll
 		for (uint32_t h = 0; h < 2u; h++) {
 			uint2 te[8];
 #pragma unroll
 			for (uint32_t jj = 0; jj < 4u; jj++) {
 				const uint32_t j = 4u * h + jj;
-				te[2 * jj] = *reinterpret_cast<const uint2 *>(tab + (q8[j] & 0xFFFFu));
-				te[2 * jj + 1] = *reinterpret_cast<const uint2 *>(tab + (q8[j] >> 16));
+				// the two table offsets 8 min(q, 17): one shift each, with the
+				// SDWA word select (the compiler masks and shifts separately)
+				uint32_t oa, ob;
+				asm("v_lshlrev_b32_sdwa %0, %2, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+				    "v_lshlrev_b32_sdwa %1, %2, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+				    : "=&v"(oa), "=&v"(ob)
+				    : "v"(3u), "v"(q8[j]));
+				te[2 * jj] = *reinterpret_cast<const uint2 *>(tab + oa);
+				te[2 * jj + 1] = *reinterpret_cast<const uint2 *>(tab + ob);
 			}
 			uint32_t lw = 0u;
 #pragma unroll
@@ -813,12 +819,13 @@ rice_kernel(KArgs a)
 				uint32_t fast = (cwa << eb.y) | cwb;
 				asm volatile("" : "+v"(fast));
 				V[c][j] = L > 32u ? m[j] : fast;
-				t += L;
 				lw = jj ? (lw | (L << (8u * jj))) : L;
 			}
 			lp[c][h] = lw;
 		}
-		T[c] = t;
+		// the chunk's bits: its eight pair lengths (bytes, each <= 64) summed
+		// by two v_sad_u8
+		T[c] = __builtin_amdgcn_sad_u8(lp[c][0], 0u, __builtin_amdgcn_sad_u8(lp[c][1], 0u, 0u));
 		// opaque: keeps the compiler from recomputing the pairs in the packer
 #pragma unroll
 		for (uint32_t j = 0; j < 8u; j++)

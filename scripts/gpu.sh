@@ -7,6 +7,7 @@
 #   bench:W          bench.py --workload W (cfg2 with the CPU baseline)
 #   kt:W             rocprofv3 kernel trace + stats of bench.py --workload W
 #   traffic:W        FETCH_SIZE and WRITE_SIZE passes (separate runs) -> traffic_W.json
+#   pmcsum:W         the two SQ counter passes over bench.py W -> pmc_summary.json (scripts/pmc_summary.py)
 #   pmc:W:C1,C2,...  one PMC pass (counters within one pass's limits) over kbench W
 #   kb:W[:LIB]       scripts/kbench.py W, cold (3 rotated sets), exp/LIB/libairscmp.so if given
 #   kbt:W[:LIB]      kb:W under a rocprofv3 kernel trace (110 launches, per-launch durations)
@@ -67,13 +68,27 @@ for st in "$@"; do
 		cut -c1-300 $O/traffic_$w.json
 		find $O -name "*.db" -delete
 		;;
+	pmcsum)
+		# the two SQ passes of the encode kernels on bench.py --workload W -> pmc_summary.json
+		B="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-warm --workload $w"
+		timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
+			SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT -d $O/pmc_${w}_1 -o p -- \
+			python3 $B >$O/pmc_${w}_1.log 2>&1 || { tail -5 $O/pmc_${w}_1.log; exit 1; }
+		timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SMEM \
+			SQ_ACTIVE_INST_SCA SQ_INST_LEVEL_LDS SQ_ACTIVE_INST_MISC -d $O/pmc_${w}_2 -o p -- \
+			python3 $B >$O/pmc_${w}_2.log 2>&1 || { tail -5 $O/pmc_${w}_2.log; exit 1; }
+		python3 scripts/pmc_summary.py $O >$O/pmc_summary_$w.json 2>$O/pmc_summary.err
+		python3 -c "import json; d=json.load(open('$O/pmc_summary_$w.json')); print(json.dumps({k: v.get('_per_sample_dominant') for k, v in d.items()})[:1500])"
+		find $O -name "*.db" -delete
+		;;
 	pmc)
-		tagp=$(echo "$x" | tr ',' '_' | cut -c1-40)
+		tagp=$(echo "$x" | tr ',' '_' | cut -c1-40)_d${AIRS_DBG:-0}
 		AIRS_KB_ROT=3 timeout -s KILL 90 rocprofv3 --pmc ${x//,/ } --output-format csv \
 			-d $O/pmc_${w}_$tagp -o p -- python3 scripts/kbench.py $w >$O/pmc_${w}_$tagp.log 2>&1 || { tail -3 $O/pmc_${w}_$tagp.log; exit 1; }
 		;;
 	kb)
-		env $(libenv "$x") AIRS_KB_ROT=3 timeout -k 10 120 python scripts/kbench.py $w >>$O/kb.jsonl 2>>$O/kb.err || { tail -3 $O/kb.err; exit 1; }
+		# kb:W[:LIB[:DBG]]  (DBG: AIRS_DBG ablation bits, ablation builds only)
+		env $(libenv "$x") ${tg:+AIRS_DBG=$tg} AIRS_KB_ROT=3 timeout -k 10 120 python scripts/kbench.py $w >>$O/kb.jsonl 2>>$O/kb.err || { tail -3 $O/kb.err; exit 1; }
 		tail -1 $O/kb.jsonl
 		;;
 	kbt)
