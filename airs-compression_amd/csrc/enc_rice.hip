@@ -528,7 +528,7 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 		sm += __shfl_xor(sm, 1, 64);
 		if (h == 0u)
 			s_hist[r] = sm;
-		static_assert(AUTO_BINS == RWG / 2u + 1u, "rows 0..127 by thread pairs, then row 128");
+		static_assert(RWG != 256u || AUTO_BINS == RWG / 2u + 1u, "rows 0..127 by thread pairs, then row 128");
 		if (wid == 0) {
 			const uint32_t s128 = wave_sum(H[128u * 64u + lane]);
 			if (lane == 0)
@@ -540,15 +540,23 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 	for (uint32_t i = tid; i < AUTO_BINS * 64u / 4u; i += RWG)
 		reinterpret_cast<uint4 *>(H)[i] = make_uint4(0u, 0u, 0u, 0u);
 	// the segment's 16 candidate sums: thread (slice sl, k) covers bins sl,
-	// sl + 16, ...; the four slices of a wave meet through two shuffles
+	// sl + 16, ...; the four slices of a wave meet through two shuffles.
+	// auto_term without branches: bin b = 8 t + f (top bit t, next three
+	// bits f) and x = (8 + f) << 4; min(v >> k, 16) summed over the bin is
+	// min(16, x >> max(k + 7 - t, 0)): 16 when k <= t - 4, 0 when k > t, the
+	// top t - k + 1 bits otherwise.  f is the thread's (sl mod 8), t grows by
+	// 2 per step.
 	{
 		const uint32_t k = tid & 15u, sl = tid >> 4;
+		const uint32_t x = (8u + (sl & 7u)) << 4;
+		const int32_t sh0 = (int32_t)k + 7 - (int32_t)(sl >> 3);
 		uint32_t part = 0u;
 #pragma unroll
 		for (uint32_t i = 0; i < (AUTO_BINS + 15u) / 16u; i++) {
 			const uint32_t b = sl + 16u * i;
-			if (b < AUTO_BINS)
-				part += s_hist[b] * auto_term(b, k);
+			const uint32_t term = min(16u, x >> (uint32_t)max(sh0 - 2 * (int32_t)i, 0));
+			if (i + 1u < (AUTO_BINS + 15u) / 16u || b < AUTO_BINS)
+				part += __umul24(s_hist[b < AUTO_BINS ? b : 0u], b < AUTO_BINS ? term : 0u); // (< 2^14 x 16)
 		}
 		part += __shfl_xor(part, 16, 64);
 		part += __shfl_xor(part, 32, 64);
@@ -1108,6 +1116,8 @@ bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s, bool stream)
 bool rice_auto_encode(const KArgs &k, uint32_t pre, hipStream_t s)
 {
 	if (pre != PRE_NONE && pre != PRE_DIFF)
+		return false;
+	if (RWG != 256u) // the histogram's row split is for 256 threads
 		return false;
 	if (!k.ktot || k.frame_g || k.model_mode || k.segs_per_frame == 0u || k.n % RSEGN)
 		return false;
