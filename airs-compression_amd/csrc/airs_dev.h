@@ -238,11 +238,12 @@ uint32_t airs_dev_patch_ids(struct airs_dev_engine *e, void *dst, uint64_t dst_s
  * AIRS_HCO_MAX_IDS frames, ids[f] for frame f).  wait polls for the signal
  * and copies the flags out (a fault count is returned as an error).
  * release MUST follow every successful begin (with ids, or NULL: no patch),
- * before any other wait on the stream; it returns 1 when the kernel patched
- * the identifiers (it waits for the kernel's acknowledgement), 0 when the
- * caller must: NULL, more than the block holds, a second release of the same
- * seq (wait released it on its time-out), or a kernel that gave up waiting
- * for the release. */
+ * before any other wait on the stream; it returns 1 when the kernel patches
+ * the identifiers, 0 when the caller must: NULL, more than the block holds, or
+ * a second release of the same seq (wait released it on its time-out).  The
+ * kernel acknowledges whether it patched; the engine checks that at the next
+ * stream wait (airs_dev_sync) or commit, and patches the headers itself when
+ * the kernel gave up waiting for the release. */
 #define AIRS_COMMIT_MAX_CTX 8192u /* contexts a commit kernel flags (AIRS_HCO_MAX_CTX) */
 uint32_t airs_dev_commit_begin(struct airs_dev_engine *e, const uint32_t *status, uint32_t num_ctx, uint32_t fpc,
 			       void *dst, uint64_t dst_stride, uint32_t *seq);

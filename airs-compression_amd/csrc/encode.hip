@@ -1177,6 +1177,20 @@ struct airs_dev_engine {
 	uint32_t hco_released;  // the last sequence word released (airs_dev_commit_release)
 	uint64_t commit_ticks;  // the commit kernel's wait for the release (100 MHz ticks)
 	uint64_t commit_polls;  // the host's wait for the commit kernel's signal (pause loops)
+	// a release with identifiers whose patch is not yet confirmed by the
+	// kernel's acknowledgement (checked at the next stream wait): its seq (0:
+	// none), the frames and the identifiers (page-locked: patch_ids_kernel
+	// reads them over the bus if the kernel gave up)
+	uint32_t commit_total;   // the frames of the commit kernel last begun
+	void *commit_dst;
+	uint64_t commit_dst_stride;
+	const uint32_t *commit_status;
+	uint32_t pend_seq, pend_total, pend_buf; // the pending release (pend_seq 0: none)
+	void *pend_dst;
+	uint64_t pend_dst_stride;
+	const uint32_t *pend_status;
+	uint64_t *commit_ids[2]; // two buffers: a patch queued for release N reads its own
+	size_t commit_ids_cap[2];
 	// cmp_gpu_engine_set_option (include/cmp_gpu.h)
 	uint32_t opt_exclusive;     // CMP_GPU_OPT_EXCLUSIVE
 	uint32_t opt_walk_segment;  // CMP_GPU_OPT_WALK_SEGMENT: 0, 2048 or 4096
@@ -1216,6 +1230,8 @@ extern "C" const char *airs_dev_last_error(void)
 {
 	return g_err;
 }
+
+static int commit_verify(struct airs_dev_engine *e);
 
 extern "C" struct airs_dev_engine *airs_dev_engine_create(void *stream)
 {
@@ -1261,6 +1277,8 @@ extern "C" void airs_dev_engine_destroy(struct airs_dev_engine *e)
 	if (!e)
 		return;
 	(void)hipStreamSynchronize(e->stream);
+	if (commit_verify(e))
+		(void)hipStreamSynchronize(e->stream);
 	(void)hipFree(e->agg);
 	(void)hipFree(e->tail);
 	(void)hipFree(e->ticket);
@@ -1271,6 +1289,9 @@ extern "C" void airs_dev_engine_destroy(struct airs_dev_engine *e)
 		(void)hipFree(e->scratch[i]);
 	if (e->pinned)
 		(void)hipHostFree(e->pinned);
+	for (int b = 0; b < 2; b++)
+		if (e->commit_ids[b])
+			(void)hipHostFree(e->commit_ids[b]);
 	if (e->hco)
 		(void)hipHostFree((void *)e->hco);
 	free(e);
@@ -2217,6 +2238,10 @@ extern "C" uint32_t airs_dev_commit_begin(struct airs_dev_engine *e, const uint3
 	if (num_ctx > AIRS_HCO_MAX_CTX)
 		return ERRV(E_PARAMS_INVALID);
 	*seq = ++e->hco_seq;
+	e->commit_dst = dst;
+	e->commit_dst_stride = dst_stride;
+	e->commit_status = status;
+	e->commit_total = num_ctx * fpc;
 	hipLaunchKernelGGL(commit_kernel, dim3(1), dim3(256), 0, e->stream, status, num_ctx, fpc, e->ticket, e->hco, *seq,
 			   (uint8_t *)dst, dst_stride, e->commit_ticks);
 	HIPCHECK(hipGetLastError());
@@ -2231,6 +2256,8 @@ extern "C" uint32_t airs_dev_commit_wait(struct airs_dev_engine *e, uint32_t seq
 {
 	for (uint64_t i = 0; i < e->commit_polls; i++) { // ~ a second of polls
 		if (e->hco[AIRS_HCO_SEQ] == seq) {
+			// the previous commit kernel ran before this one: its acknowledgement is final
+			commit_verify(e);
 			const uint32_t faults = e->hco[AIRS_HCO_FAULT];
 			memcpy(flags, (const void *)((const volatile uint8_t *)e->hco + AIRS_HCO_FLAGS), num_ctx);
 			if (faults) {
@@ -2254,11 +2281,12 @@ extern "C" uint32_t airs_dev_commit_wait(struct airs_dev_engine *e, uint32_t seq
 	return 0;
 }
 
-// Release the commit kernel of `seq`: 1 when it patched the identifiers
-// (ids given, and the kernel acknowledged a patch), 0 when the caller must
-// patch them: no ids, a second release of the same seq (commit_wait released
-// it already, with mode 0), or a kernel that gave up waiting before the
-// release came (its acknowledgement says it did not patch).
+// Release the commit kernel of `seq`: 1 when it patches the identifiers
+// (ids given: the engine checks the kernel's acknowledgement at the next
+// stream wait or commit, and patches the headers itself if the kernel gave
+// up waiting for this release), 0 when the caller must patch them
+// (no ids, more than the block holds, or a second release of the same seq:
+// commit_wait released it on its time-out, with mode 0).
 extern "C" int airs_dev_commit_release(struct airs_dev_engine *e, uint32_t seq, const uint64_t *ids, uint32_t total)
 {
 	if (e->hco_released == seq)
@@ -2266,31 +2294,58 @@ extern "C" int airs_dev_commit_release(struct airs_dev_engine *e, uint32_t seq, 
 	e->hco_released = seq;
 	if (ids && total > AIRS_HCO_MAX_IDS)
 		ids = nullptr;
-	if (ids)
+	const uint32_t b = seq & 1u;
+	if (ids && e->commit_ids_cap[b] < total) {
+		if (e->commit_ids[b])
+			(void)hipHostFree(e->commit_ids[b]);
+		e->commit_ids[b] = nullptr;
+		e->commit_ids_cap[b] = 0;
+		if (hipHostMalloc((void **)&e->commit_ids[b], (size_t)total * 8u, hipHostMallocDefault) == hipSuccess)
+			e->commit_ids_cap[b] = total;
+		else
+			ids = nullptr; // (the caller patches)
+	}
+	if (ids) {
 		memcpy((void *)((volatile uint8_t *)e->hco + AIRS_HCO_IDS), ids, (size_t)total * 8u);
+		memcpy(e->commit_ids[b], ids, (size_t)total * 8u);
+		e->pend_seq = seq;
+		e->pend_total = total;
+		e->pend_buf = b;
+		e->pend_dst = e->commit_dst;
+		e->pend_dst_stride = e->commit_dst_stride;
+		e->pend_status = e->commit_status;
+	}
 	e->hco[AIRS_HCO_MODE] = ids ? 1u : 0u;
 	__atomic_thread_fence(__ATOMIC_SEQ_CST);
 	e->hco[AIRS_HCO_GO] = seq;
-	if (!ids)
+	return ids ? 1 : 0;
+}
+
+// The pending release's acknowledgement, once its commit kernel has ended
+// (after a stream wait, or once the next commit kernel has signalled): a
+// kernel that gave up before the release came left the headers alone, so
+// the identifiers are patched here (queued on the stream; sync_wait waits
+// for it).  Returns 1 when a patch was queued.
+static int commit_verify(struct airs_dev_engine *e)
+{
+	if (!e->pend_seq)
 		return 0;
-	// the kernel signalled (commit_wait) and is waiting or has given up: its
-	// acknowledgement follows within its patch time
-	const uint32_t want = (seq & 0x7FFFFFFFu) << 1;
-	for (uint64_t i = 0; i < e->commit_polls + 1024u; i++) {
-		const uint32_t ack = e->hco[AIRS_HCO_ACK];
-		if ((ack & ~1u) == want)
-			return (int)(ack & 1u);
-		__builtin_ia32_pause();
-	}
-	if (sync_wait(e, false)) // the kernel has ended (or the stream faulted)
+	const uint32_t seq = e->pend_seq, ack = e->hco[AIRS_HCO_ACK];
+	e->pend_seq = 0u;
+	if ((ack & ~1u) == ((seq & 0x7FFFFFFFu) << 1) && (ack & 1u))
 		return 0;
-	const uint32_t ack = e->hco[AIRS_HCO_ACK];
-	return (ack & ~1u) == want ? (int)(ack & 1u) : 0;
+	// (the next write of this buffer is release seq + 2, after this patch ran)
+	hipLaunchKernelGGL(patch_ids_kernel, dim3((e->pend_total + 255u) / 256u), dim3(256), 0, e->stream,
+			   (uint8_t *)e->pend_dst, e->pend_dst_stride, e->pend_total, 0u, 1u,
+			   (const uint64_t *)e->commit_ids[e->pend_buf], e->pend_status);
+	return hipGetLastError() == hipSuccess ? 1 : 0;
 }
 
 static uint32_t sync_wait(struct airs_dev_engine *e, bool waited)
 {
 	if (!waited)
+		HIPCHECK(hipStreamSynchronize(e->stream));
+	if (commit_verify(e)) // a commit kernel gave up: the headers patched from here
 		HIPCHECK(hipStreamSynchronize(e->stream));
 	const uint32_t faults = e->hco[AIRS_HCO_FAULT];
 #if AIRS_ABLATE
