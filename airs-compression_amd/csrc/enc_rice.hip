@@ -18,7 +18,11 @@
 //     the code-table offsets: 40 registers per lane for the segment's 64
 //     samples instead of 64.  The table lookups move into phase 1, where
 //     they overlap the sample loads of the other workgroups; the packer
-//     reads no LDS at all.  (Five workgroups per CU would fit the registers,
+//     reads no LDS at all.  Round 6: one lookup per PAIR, in a table of
+//     the 18 x 18 (min(q_a, 17), min(q_b, 17)) combinations holding
+//     P = (T'[q_a] << l_b) + T'[q_b] and the lengths, so that V =
+//     (m_a << l_b) + m_b + P (15 VALU per pair instead of 18, 65 VGPRs
+//     instead of 80);  (Five workgroups per CU would fit the registers,
 //     but the look-back chains then stall: four);
 //   * the segment is packed back to back into ONE arena sized for a
 //     compressed segment (~15.7 bits per sample; a segment that does not
@@ -44,15 +48,16 @@ namespace airs {
 #define AIRS_RICE_WG 256
 #endif
 // workgroups per CU the LDS arena (and the register allocation) is sized
-// for: DIFF frames 6 (round 6: with the scalar look-back the chains no
-// longer stall at more than four; cfg2 53.0-53.9 -> 50.1-53.5 us, with the
-// nt stores 47.8-51.2), NONE 5 (at 6 its registers spill to scratch), AUTO 4
-// (its mapped samples stay live across the candidate barrier: 99 VGPRs)
+// for: DIFF and NONE frames 6 (round 6: with the scalar look-back the chains
+// no longer stall at more than four; cfg2 53.0-53.9 -> 50.1-53.5 us, with
+// the nt stores 47.8-51.2; the pair table took the kernel from 80 to 65
+// VGPRs, and 7 or 8 per CU measured the same as 6), AUTO 4 (its mapped
+// samples stay live across the candidate barrier: 99 VGPRs)
 #ifndef AIRS_RICE_WGPCU
 #define AIRS_RICE_WGPCU 6
 #endif
 #ifndef AIRS_RICE_NONE_WGPCU
-#define AIRS_RICE_NONE_WGPCU 5
+#define AIRS_RICE_NONE_WGPCU 6
 #endif
 #ifndef AIRS_RICE_AUTO_WGPCU
 #define AIRS_RICE_AUTO_WGPCU 4
@@ -78,7 +83,7 @@ constexpr uint32_t RSEGN = RCH * RCHUNK;    // samples per segment (16 Ki or 32 
 constexpr uint32_t RGUARD = 4u;              // words before the arena (a lane's first put ORs zeros there)
 // LDS per workgroup is allocated in granules: leave room for the static LDS
 // and the rounding (measured: a 32464-byte workgroup admitted only four per CU)
-constexpr uint32_t RSTATIC = 2048u;
+constexpr uint32_t RSTATIC = 2048u + 18u * 18u * 8u; // (+ the pair table)
 
 template <int PRE, bool AUTO>
 __host__ __device__ constexpr uint32_t rice_wgpcu()
@@ -631,6 +636,18 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 	return make_uint2(__builtin_amdgcn_readfirstlane(s_res[0]), __builtin_amdgcn_readfirstlane(s_res[1]));
 }
 
+// The pair table (rice_kernel's s_ptab) for k: 324 entries by the whole
+// workgroup (before B0)
+__device__ __forceinline__ void rice_pair_table(uint2 *pt, uint32_t k, uint32_t tid)
+{
+	for (uint32_t i = tid; i < 18u * 18u; i += RWG) {
+		const uint32_t qa = i / 18u, qb = i - 18u * qa;
+		const uint2 ea = rice_table_entry(qa, k), eb = rice_table_entry(qb, k);
+		const uint32_t P = (uint32_t)((uint64_t)ea.x << eb.y) + eb.x; // (mod 2^32; exact when L <= 32)
+		pt[i] = make_uint2(P, eb.y | ((ea.y + eb.y) << 8));
+	}
+}
+
 // the lane's samples of segment `sif` of a frame: 4 chunks x 16 samples, and
 // for DIFF the sample before each chunk's first (lane 0 of each wave uses it;
 // every lane loads, so the load needs no branch; 0 before the frame's first
@@ -676,6 +693,10 @@ rice_kernel(KArgs a)
 	constexpr uint32_t HDR_BITS = STREAM ? 0u : 176u;
 	extern __shared__ __attribute__((aligned(16))) uint32_t L_ar[]; // RGUARD words, then the arena
 	__shared__ __attribute__((aligned(16))) uint2 s_tab[20];
+	// the pair table: entry 18 qa + qb (qa, qb = min(q, 17) of a sample pair)
+	// = (P, lb | L << 8): P = (T'[qa] << lb) + T'[qb], lb the second code's
+	// length, L the pair's (P meaningless when L > 32)
+	__shared__ __attribute__((aligned(16))) uint2 s_ptab[18 * 18];
 	__shared__ __attribute__((aligned(16))) uint32_t s_wsum[2][RNW];
 	__shared__ uint32_t s_misc[4];
 
@@ -749,13 +770,15 @@ rice_kernel(KArgs a)
 		cd = make_coder<ENC_ZERO>(1u << k, a.outlier_param);
 		if (tid < 18u)
 			s_tab[tid] = rice_table_entry(tid, k);
-		__syncthreads(); // the table; the arena is zero again (rice_auto_k)
+		rice_pair_table(s_ptab, k, tid);
+		__syncthreads(); // the tables; the arena is zero again (rice_auto_k)
 	} else {
 		cd = make_coder<ENC_ZERO>(__builtin_amdgcn_readfirstlane(a.g), a.outlier_param);
 		k = cd.k;
 		if (tid < 18u)
 			s_tab[tid] = rice_table_entry(tid, k);
-		__syncthreads(); // B0: table and zeroed arena
+		rice_pair_table(s_ptab, k, tid);
+		__syncthreads(); // B0: tables and zeroed arena
 	}
 
 	// ---- phase 1: codeword pairs and lengths -----------------------------
@@ -763,7 +786,8 @@ rice_kernel(KArgs a)
 	// back (or the two mapped values when they exceed 32 bits); lp[c]: the
 	// eight pair lengths, a byte each; T[c]: their sum
 	uint32_t V[RCH][8], lp[RCH][2], T[RCH];
-	const char *tab = reinterpret_cast<const char *>(s_tab);
+	const char *ptab = reinterpret_cast<const char *>(s_ptab);
+	const uint32_t c32 = 32u;
 #pragma unroll
 	for (uint32_t c = 0; c < RCH; c++) {
 		const uint32_t w[8] = {raw[c][0].x, raw[c][0].y, raw[c][0].z, raw[c][0].w,
@@ -802,32 +826,45 @@ rice_kernel(KArgs a)
 		}
 #pragma unroll
 		for (uint32_t h = 0; h < 2u; h++) {
-			uint2 te[8];
+			// one pair-table read per pair: its byte offset 144 qa + 8 qb by
+			// one v_dot2 of the packed min(q, 17)
+			uint2 te[4];
 #pragma unroll
 			for (uint32_t jj = 0; jj < 4u; jj++) {
-				const uint32_t j = 4u * h + jj;
-				// the two table offsets 8 min(q, 17): one shift each, with the
-				// SDWA word select (the compiler masks and shifts separately)
-				uint32_t oa, ob;
-				asm("v_lshlrev_b32_sdwa %0, %2, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
-				    "v_lshlrev_b32_sdwa %1, %2, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
-				    : "=&v"(oa), "=&v"(ob)
-				    : "v"(3u), "v"(q8[j]));
-				te[2 * jj] = *reinterpret_cast<const uint2 *>(tab + oa);
-				te[2 * jj + 1] = *reinterpret_cast<const uint2 *>(tab + ob);
+				const uint32_t ofs = __builtin_amdgcn_udot2(pk(q8[4u * h + jj]), (u16x2){144, 8}, 0u, false);
+				te[jj] = *reinterpret_cast<const uint2 *>(ptab + ofs);
 			}
 			uint32_t lw = 0u;
 #pragma unroll
 			for (uint32_t jj = 0; jj < 4u; jj++) {
 				const uint32_t j = 4u * h + jj;
-				const uint2 ea = te[2 * jj], eb = te[2 * jj + 1];
-				const uint32_t cwa = (m[j] & 0xFFFFu) + ea.x, cwb = (m[j] >> 16) + eb.x;
-				const uint32_t L = ea.y + eb.y;
-				// (computed for every pair: a select, not a branch)
-				uint32_t fast = (cwa << eb.y) | cwb;
+				const uint2 e = te[jj];
+				// the codeword pair (m_a << lb) + m_b + P, with the halves of m
+				// selected by SDWA
+				uint32_t t1, t2, v;
+				asm("v_lshlrev_b32_sdwa %0, %2, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+				    "v_add_u32_sdwa %1, %4, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+				    : "=&v"(t1), "=&v"(t2)
+				    : "v"(e.y), "v"(m[j]), "v"(e.x));
+				uint32_t fast = t1 + t2;
 				asm volatile("" : "+v"(fast));
-				V[c][j] = L > 32u ? m[j] : fast;
-				lw = jj ? (lw | (L << (8u * jj))) : L;
+				// pairs of more than 32 bits keep their mapped values (L > 32:
+				// an SDWA compare of the length byte)
+				asm("v_cmp_lt_u32_sdwa vcc, %3, %4 src0_sel:DWORD src1_sel:BYTE_1\n\t"
+				    "v_cndmask_b32 %0, %1, %2, vcc"
+				    : "=v"(v)
+				    : "v"(fast), "v"(m[j]), "v"(c32), "v"(e.y)
+				    : "vcc");
+				V[c][j] = v;
+				// the length byte into byte jj of lw
+				if (jj == 0u)
+					asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(lw) : "v"(e.y));
+				else if (jj == 1u)
+					asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(lw) : "v"(e.y));
+				else if (jj == 2u)
+					asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(lw) : "v"(e.y));
+				else
+					asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(lw) : "v"(e.y));
 			}
 			lp[c][h] = lw;
 		}

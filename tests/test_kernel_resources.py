@@ -20,13 +20,13 @@ LIB = os.path.join(PKG_DIR, "lib", "libairscmp.so")
 # symbol: (max VGPRs, max SGPR spills to VGPR lanes); VGPR spills must be 0
 BUDGETS = {
     # cfg2 / cfg4: the Rice/ZERO frame kernel (enc_rice.hip), DIFF and NONE:
-    # six (DIFF) and five (NONE) workgroups per CU since round 6: <= 85 and
-    # <= 102 VGPRs
+    # six workgroups per CU since round 6: <= 85 VGPRs (65 with the pair
+    # table of round 6)
     # (round 6: the scalar look-back of XCD-local frames, rice_lookback_s,
     # holds a 16-granule window in 32 SGPRs: 19 spills to VGPR lanes, all in
     # wave 0's look-back, once per segment)
     "_ZN4airs11rice_kernelILi1ELb0ELb0EEEvNS_5KArgsE": (85, 24),
-    "_ZN4airs11rice_kernelILi0ELb0ELb0EEEvNS_5KArgsE": (102, 24),
+    "_ZN4airs11rice_kernelILi0ELb0ELb0EEEvNS_5KArgsE": (85, 24),
     "_ZN4airs11rice_kernelILi1ELb1ELb0EEEvNS_5KArgsE": (85, 0),
     # cfg3: the Rice kernel with the frame's k chosen in it (AUTO; round 6):
     # the 64 mapped samples stay in registers across the candidate barrier
