@@ -578,6 +578,7 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 				sk += s_kt[w][lane];
 			gran_store(&a.ktot[(uint64_t)gseg * 16u + lane], ((uint64_t)a.epoch << 32) | sk);
 		}
+		dbg_stamp(a, gseg, 5); // (AUTO: candidates published)
 		const uint32_t first_seg = gseg - sif, ng = a.segs_per_frame * 16u;
 		constexpr uint32_t NL = (AUTO_MAX_SPF + 3u) / 4u; // granule loads per lane
 		uint64_t gk[NL];
@@ -606,6 +607,7 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 					gk[i] = gran_load(&a.ktot[(uint64_t)first_seg * 16u + gi]);
 			}
 		}
+		dbg_stamp(a, gseg, 6); // (AUTO: every candidate of the frame seen)
 		// lane l holds segment 4 i + l / 16, candidate k = l % 16
 		uint32_t tot = 0u, pre = 0u;
 #pragma unroll

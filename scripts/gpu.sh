@@ -107,7 +107,12 @@ for st in "$@"; do
 		python3 scripts/launch_stats.py $d/kt_kernel_trace.csv $(kern $w)
 		spf=256
 		[ "$w" = cfg4 ] && spf=4
-		python3 scripts/ts_launches.py $d.bin $((110 + ${AIRS_KB_PRE:-0})) $spf >$d.txt 2>&1
+		if [ "$w" = cfg3 ]; then
+			python3 scripts/ts_auto.py $d.bin $((110 + ${AIRS_KB_PRE:-0})) >$d.txt 2>&1
+		else
+			python3 scripts/ts_launches.py $d.bin $((110 + ${AIRS_KB_PRE:-0})) $spf >$d.txt 2>&1
+		fi
+		head -12 $d.txt
 		gzip $d.bin
 		;;
 	run)
