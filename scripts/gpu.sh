@@ -56,6 +56,10 @@ for st in "$@"; do
 		timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$w -o kt -- python3 bench.py \
 			--workload $w --no-cpu-baseline --no-warm >$O/kt_$w.log 2>&1 || { tail $O/kt_$w.log; exit 1; }
 		python3 scripts/launch_stats.py $O/kt_$w/kt_kernel_trace.csv $(kern $w)
+		# the 25 launches after bench.py's 5 untimed warmups (its 20 timed steps
+		# and the first 5 of its separate per-launch pass)
+		python3 scripts/launch_stats.py $O/kt_$w/kt_kernel_trace.csv $(kern $w) --skip 5 --count 25 \
+			--json $O/kt_${w}_launches.json
 		;;
 	traffic)
 		K=$(kern $w)
