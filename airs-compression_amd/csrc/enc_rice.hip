@@ -1134,9 +1134,11 @@ bool rice_encode(const KArgs &k, uint32_t pre, hipStream_t s, bool stream)
 	// value is true wherever it runs, and the vector look-back takes over
 	// after AIRS_RICE_SPOLL scalar polls)
 	ka.lbmode = !stream && nfr % 8u == 0u ? 1u : 0u;
-	static const char *lbm = getenv("AIRS_RICE_LBMODE"); // benchmarking override
+#if AIRS_ABLATE
+	static const char *lbm = getenv("AIRS_RICE_LBMODE"); // (ablation builds: the look-back mode)
 	if (lbm)
 		ka.lbmode = (uint32_t)atoi(lbm);
+#endif
 	const size_t lds = (size_t)ka.img_words * 4u;
 	void (*kern)(KArgs);
 	if (stream)
