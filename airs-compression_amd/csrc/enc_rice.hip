@@ -216,7 +216,7 @@ __device__ __forceinline__ uint2 lb_resolve(const KArgs &a, uint32_t gseg, uint3
 		__builtin_amdgcn_s_sleep(1);
 		tv = gran_load(&a.tail[gseg - 1u]);
 	}
-	if (DBG(65536u) && a.dbgts && lane == 0) {
+	if (DBG(65536u) && !DBG(262144u) && a.dbgts && lane == 0) {
 		a.dbgts[8u * gseg + 5u] = ((uint64_t)spins << 32) | rounds;
 		a.dbgts[8u * gseg + 6u] = s2;
 	}
@@ -398,7 +398,7 @@ __device__ __forceinline__ uint2 rice_lookback_s(const KArgs &a, uint32_t gseg, 
 			     : "memory");
 		have_tail = (uint32_t)(tv >> 32) == epoch;
 	}
-	if (DBG(65536u) && a.dbgts && lane == 0) {
+	if (DBG(65536u) && !DBG(262144u) && a.dbgts && lane == 0) {
 		a.dbgts[8u * gseg + 5u] = ((uint64_t)polls << 32) | rounds;
 		a.dbgts[8u * gseg + 6u] = 0u;
 	}
@@ -642,11 +642,16 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 // workgroup (before B0)
 __device__ __forceinline__ void rice_pair_table(uint2 *pt, uint32_t k, uint32_t tid)
 {
+	// T'[q] in 32 bits (q + k <= 31: 2 << 31 wraps to the right residue)
+	auto ent = [k](uint32_t q) {
+		return q >= 17u ? make_uint2(0u, k + 17u)
+				: make_uint2((2u << (q + k)) - (2u << k) - (q << k) + 1u, k + 1u + q);
+	};
 	for (uint32_t i = tid; i < 18u * 18u; i += RWG) {
-		const uint32_t qa = i / 18u, qb = i - 18u * qa;
-		const uint2 ea = rice_table_entry(qa, k), eb = rice_table_entry(qb, k);
-		const uint32_t P = (uint32_t)((uint64_t)ea.x << eb.y) + eb.x; // (mod 2^32; exact when L <= 32)
-		pt[i] = make_uint2(P, eb.y | ((ea.y + eb.y) << 8));
+		const uint32_t qa = __umul24(i, 3641u) >> 16, qb = i - 18u * qa; // (i / 18 for i < 324)
+		const uint2 ea = ent(qa), eb = ent(qb);
+		// (mod 2^32; exact when L <= 32, meaningless otherwise, e.g. l_b = 32)
+		pt[i] = make_uint2((ea.x << (eb.y & 31u)) + eb.x, eb.y | ((ea.y + eb.y) << 8));
 	}
 }
 
@@ -736,10 +741,19 @@ rice_kernel(KArgs a)
 	uint4 raw[RCH][2];
 	uint32_t prevld[RCH];
 	rice_load<PRE>(a, fsrc, sif, gseg, tid, raw, prevld);
+	if (DBG(262144u)) { // ablation timeline: slot 5 = wave 0's samples landed, 6 = phase 1 done
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		if (wid == 0)
+			dbg_stamp(a, gseg, 5);
+	}
 	{
+		// (the arena size is the launch's, a compile-time constant: an unrolled loop)
+		constexpr uint32_t IW = rice_arena_words(rice_wgpcu<PRE, AUTO>());
 		uint4 *L4 = reinterpret_cast<uint4 *>(L_ar);
-		for (uint32_t i = tid; i < a.img_words / 4u; i += RWG)
-			L4[i] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+		for (uint32_t i = 0; i < (IW / 4u + RWG - 1u) / RWG; i++)
+			if (i * RWG + tid < IW / 4u)
+				L4[i * RWG + tid] = make_uint4(0u, 0u, 0u, 0u);
 	}
 	const bool is_first = sif == 0u, is_last = sif + 1u == a.segs_per_frame;
 	Coder cd;
@@ -879,6 +893,8 @@ rice_kernel(KArgs a)
 			asm volatile("" : "+v"(V[c][j]));
 	}
 
+	if (DBG(262144u) && wid == 0)
+		dbg_stamp(a, gseg, 6);
 	// ---- block scan of the chunk totals (two chunks per register: a wave's
 	// inclusive sums stay below 2^16) --------------------------------------
 	const uint32_t inc01 = wave_incl_scan(T[0] | (T[1] << 16));
