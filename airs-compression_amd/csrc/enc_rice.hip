@@ -803,7 +803,6 @@ rice_kernel(KArgs a)
 	// eight pair lengths, a byte each; T[c]: their sum
 	uint32_t V[RCH][8], lp[RCH][2], T[RCH];
 	const char *ptab = reinterpret_cast<const char *>(s_ptab);
-	const uint32_t c32 = 32u;
 #pragma unroll
 	for (uint32_t c = 0; c < RCH; c++) {
 		const uint32_t w[8] = {raw[c][0].x, raw[c][0].y, raw[c][0].z, raw[c][0].w,
@@ -864,13 +863,10 @@ rice_kernel(KArgs a)
 				    : "v"(e.y), "v"(m[j]), "v"(e.x));
 				uint32_t fast = t1 + t2;
 				asm volatile("" : "+v"(fast));
-				// pairs of more than 32 bits keep their mapped values (L > 32:
-				// an SDWA compare of the length byte)
-				asm("v_cmp_lt_u32_sdwa vcc, %3, %4 src0_sel:DWORD src1_sel:BYTE_1\n\t"
-				    "v_cndmask_b32 %0, %1, %2, vcc"
-				    : "=v"(v)
-				    : "v"(fast), "v"(m[j]), "v"(c32), "v"(e.y)
-				    : "vcc");
+				// pairs of more than 32 bits keep their mapped values: L > 32 is
+				// e.y > 0x20FF (l_b < 256), one plain compare (an SDWA compare
+				// issues at about half the rate under load, scripts/valu_bench.hip)
+				v = e.y > 0x20FFu ? m[j] : fast;
 				V[c][j] = v;
 				// the length byte into byte jj of lw
 				if (jj == 0u)
