@@ -22,14 +22,18 @@
 //     the 18 x 18 (min(q_a, 17), min(q_b, 17)) combinations holding
 //     P = (T'[q_a] << l_b) + T'[q_b] and the lengths, so that V =
 //     (m_a << l_b) + m_b + P (15 VALU per pair instead of 18, 65 VGPRs
-//     instead of 80);  (Five workgroups per CU would fit the registers,
-//     but the look-back chains then stall: four);
+//     instead of 80; six workgroups per CU);
 //   * the segment is packed back to back into ONE arena sized for a
-//     compressed segment (~15.7 bits per sample; a segment that does not
-//     fit is packed and stored chunk by chunk), so there is no image
-//     rotation: three barriers per segment (encode_kernel: seven);
+//     compressed segment (~11 bits per sample at six workgroups per CU; a
+//     segment that does not fit is packed and stored chunk by chunk), so
+//     there is no image rotation: three barriers per segment (encode_kernel:
+//     seven);
 //   * the look-back is evaluated once the whole segment is packed, so its
-//     predecessors published their aggregates long before (no retries).
+//     predecessors published their aggregates long before (no retries); for
+//     frames whose segments all run on one XCD its polls are scalar loads
+//     (rice_lookback_s).
+// AUTO (cfg3): the frame's k is chosen in the kernel from a histogram and a
+// candidate barrier (rice_auto_k) before phase 1; no look-back.
 // A pair whose two codewords exceed 32 bits (two zero escapes, or one
 // escape next to a long code) keeps its mapped values in V; the packer
 // re-codes it from the table in a wave-uniform slow step.
