@@ -55,8 +55,9 @@ namespace airs {
 // for: DIFF and NONE frames 6 (round 6: with the scalar look-back the chains
 // no longer stall at more than four; cfg2 53.0-53.9 -> 50.1-53.5 us, with
 // the nt stores 47.8-51.2; the pair table took the kernel from 80 to 65
-// VGPRs, and 7 or 8 per CU measured the same as 6), AUTO 4 (its mapped
-// samples stay live across the candidate barrier: 99 VGPRs)
+// VGPRs, and 7 or 8 per CU measured the same as 6), AUTO 5 (its mapped
+// samples stay live across the candidate barrier; 62 VGPRs since the
+// barrier polls one granule per lane at a time, 99 before; 5 beat 4 and 6)
 #ifndef AIRS_RICE_WGPCU
 #define AIRS_RICE_WGPCU 6
 #endif
@@ -64,7 +65,13 @@ namespace airs {
 #define AIRS_RICE_NONE_WGPCU 6
 #endif
 #ifndef AIRS_RICE_AUTO_WGPCU
-#define AIRS_RICE_AUTO_WGPCU 4
+#define AIRS_RICE_AUTO_WGPCU 5
+#endif
+// AUTO histogram counters per bin: 64 (one per lane) or 32 (lanes l and
+// l + 32 share one, two-way atomic conflicts: half the LDS, so that the
+// histogram fits the arena of five workgroups per CU)
+#ifndef AIRS_RICE_AUTO_HCOLS
+#define AIRS_RICE_AUTO_HCOLS 32
 #endif
 #ifndef AIRS_RICE_LBC // the look-back is evaluated after packing this many chunks (wave 0)
 #define AIRS_RICE_LBC 4
@@ -492,10 +499,12 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 	__shared__ uint32_t s_hist[AUTO_BINS];
 	__shared__ uint32_t s_kt[RNW][16];
 	__shared__ uint32_t s_res[2];
-	// this lane's counter of bin b is at byte hbase + 256 (b + 1016): the bin's
-	// offset comes from the float bits with one shift and one shift-add (the
-	// 32-bit LDS address arithmetic wraps)
-	const uint32_t hbase = (uint32_t)(uintptr_t)H + 4u * lane - 1016u * 256u;
+	// this lane's counter of bin b is at byte hbase + 4 HC (b + 1016): the
+	// bin's offset comes from the float bits with one shift and one shift-add
+	// (the 32-bit LDS address arithmetic wraps)
+	constexpr uint32_t HC = AIRS_RICE_AUTO_HCOLS, HSH = HC == 64u ? 8u : 7u;
+	static_assert(HC == 64u || HC == 32u, "64 or 32 counters per bin");
+	const uint32_t hbase = (uint32_t)(uintptr_t)H + 4u * (lane & (HC - 1u)) - 1016u * 4u * HC;
 	__syncthreads(); // the arena is zeroed
 #pragma unroll
 	for (uint32_t c = 0; c < RCH; c++) {
@@ -509,27 +518,28 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 			for (uint32_t h = 0; h < 2; h++) {
 				const uint32_t v = (h ? wv >> 16 : wv & 0xFFFFu) + 1u;
 				uint32_t ha;
-				asm("v_lshrrev_b32 %0, 20, %1\n\tv_lshl_add_u32 %0, %0, 8, %2"
+				asm("v_lshrrev_b32 %0, 20, %1\n\tv_lshl_add_u32 %0, %0, %3, %2"
 				    : "=&v"(ha)
-				    : "v"(__float_as_uint((float)v)), "v"(hbase));
+				    : "v"(__float_as_uint((float)v)), "v"(hbase), "i"(HSH));
 				__hip_atomic_fetch_add(reinterpret_cast<lds_u32 *>((uintptr_t)ha), 1u, __ATOMIC_RELAXED,
 						       __HIP_MEMORY_SCOPE_WORKGROUP);
 			}
 		}
 	}
 	__syncthreads();
-	// bin totals: threads 2r, 2r + 1 sum the halves of row r < 128 with eight
-	// 16-byte reads each, rotated by r (4-way bank sharing); wave 0 row 128
+	// bin totals: threads 2r, 2r + 1 sum the halves of row r < 128 with
+	// HC / 8 16-byte reads each, rotated by r (bank sharing); wave 0 row 128
 	{
+		constexpr uint32_t NQ = HC / 8u; // 16-byte reads per half row
 		const uint32_t r = tid >> 1, h = tid & 1u;
-		const uint4 *row = reinterpret_cast<const uint4 *>(H + r * 64u + h * 32u);
+		const uint4 *row = reinterpret_cast<const uint4 *>(H + r * HC + h * (HC / 2u));
 		uint32_t sm = 0u;
 #pragma unroll
-		for (uint32_t hq = 0; hq < 8u; hq += 4u) {
+		for (uint32_t hq = 0; hq < NQ; hq += 4u) {
 			uint4 q4[4];
 #pragma unroll
 			for (uint32_t q = 0; q < 4u; q++)
-				q4[q] = row[(hq + q + r) & 7u];
+				q4[q] = row[(hq + q + r) & (NQ - 1u)];
 #pragma unroll
 			for (uint32_t q = 0; q < 4u; q++)
 				sm += q4[q].x + q4[q].y + q4[q].z + q4[q].w;
@@ -539,14 +549,14 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 			s_hist[r] = sm;
 		static_assert(RWG != 256u || AUTO_BINS == RWG / 2u + 1u, "rows 0..127 by thread pairs, then row 128");
 		if (wid == 0) {
-			const uint32_t s128 = wave_sum(H[128u * 64u + lane]);
+			const uint32_t s128 = wave_sum(lane < HC ? H[128u * HC + lane] : 0u);
 			if (lane == 0)
 				s_hist[128] = s128;
 		}
 	}
 	__syncthreads();
 	// the arena again as the arena: clear the histogram rows
-	for (uint32_t i = tid; i < AUTO_BINS * 64u / 4u; i += RWG)
+	for (uint32_t i = tid; i < AUTO_BINS * HC / 4u; i += RWG)
 		reinterpret_cast<uint4 *>(H)[i] = make_uint4(0u, 0u, 0u, 0u);
 	// the segment's 16 candidate sums: thread (slice sl, k) covers bins sl,
 	// sl + 16, ...; the four slices of a wave meet through two shuffles.
@@ -584,43 +594,34 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 		}
 		dbg_stamp(a, gseg, 5); // (AUTO: candidates published)
 		const uint32_t first_seg = gseg - sif, ng = a.segs_per_frame * 16u;
-		constexpr uint32_t NL = (AUTO_MAX_SPF + 3u) / 4u; // granule loads per lane
-		uint64_t gk[NL];
-#pragma unroll
-		for (uint32_t i = 0; i < NL; i++) {
+		// 64 granules per round (one per lane), the rounds one after another
+		// so that no window of granules stays live beside the mapped pairs
+		// (cfg3's frames: one round)
+		uint32_t tot = 0u, pre = 0u, spins = 0u;
+		const uint32_t nit = (ng + 63u) / 64u;
+		for (uint32_t i = 0; i < nit; i++) {
 			const uint32_t gi = 64u * i + lane;
-			gk[i] = gi < ng ? gran_load(&a.ktot[(uint64_t)first_seg * 16u + gi]) : 0ull;
-		}
-		for (uint32_t spins = 0;;) {
-			bool bad = false;
-#pragma unroll
-			for (uint32_t i = 0; i < NL; i++)
-				bad |= 64u * i + lane < ng && (uint32_t)(gk[i] >> 32) != a.epoch;
-			if (!__ballot(bad))
-				break;
-			if (++spins > AIRS_SPIN_LIMIT) {
-				if (lane == 0)
-					atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
-				break;
+			const uint64_t *gp = &a.ktot[(uint64_t)first_seg * 16u + (gi < ng ? gi : 0u)];
+			uint64_t g = gran_load(gp);
+			for (;;) {
+				const bool bad = gi < ng && (uint32_t)(g >> 32) != a.epoch;
+				if (!__ballot(bad))
+					break;
+				if (++spins > AIRS_SPIN_LIMIT) {
+					if (lane == 0)
+						atomicAdd(a.ticket + AIRS_FAULT_WORD, 1u);
+					break;
+				}
+				__builtin_amdgcn_s_sleep(1);
+				if (bad)
+					g = gran_load(gp);
 			}
-			__builtin_amdgcn_s_sleep(1);
-#pragma unroll
-			for (uint32_t i = 0; i < NL; i++) {
-				const uint32_t gi = 64u * i + lane;
-				if (gi < ng && (uint32_t)(gk[i] >> 32) != a.epoch)
-					gk[i] = gran_load(&a.ktot[(uint64_t)first_seg * 16u + gi]);
-			}
-		}
-		dbg_stamp(a, gseg, 6); // (AUTO: every candidate of the frame seen)
-		// lane l holds segment 4 i + l / 16, candidate k = l % 16
-		uint32_t tot = 0u, pre = 0u;
-#pragma unroll
-		for (uint32_t i = 0; i < NL; i++) {
-			const uint32_t gi = 64u * i + lane;
-			const uint32_t v = gi < ng ? (uint32_t)gk[i] : 0u;
+			// lane l holds segment 4 i + l / 16, candidate k = l % 16
+			const uint32_t v = gi < ng ? (uint32_t)g : 0u;
 			tot += v;
 			pre += (gi >> 4) < sif ? v : 0u;
 		}
+		dbg_stamp(a, gseg, 6); // (AUTO: every candidate of the frame seen)
 		tot += __shfl_xor(tot, 16, 64);
 		tot += __shfl_xor(tot, 32, 64);
 		pre += __shfl_xor(pre, 16, 64);

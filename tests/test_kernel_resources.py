@@ -29,9 +29,11 @@ BUDGETS = {
     "_ZN4airs11rice_kernelILi0ELb0ELb0EEEvNS_5KArgsE": (85, 24),
     "_ZN4airs11rice_kernelILi1ELb1ELb0EEEvNS_5KArgsE": (85, 0),
     # cfg3: the Rice kernel with the frame's k chosen in it (AUTO; round 6):
-    # the 64 mapped samples stay in registers across the candidate barrier
-    "_ZN4airs11rice_kernelILi1ELb0ELb1EEEvNS_5KArgsE": (112, 0),
-    "_ZN4airs11rice_kernelILi0ELb0ELb1EEEvNS_5KArgsE": (112, 0),
+    # the 64 mapped samples stay in registers across the candidate barrier;
+    # five workgroups per CU: <= 96 VGPRs (62 since the barrier's granules
+    # are polled one per lane at a time)
+    "_ZN4airs11rice_kernelILi1ELb0ELb1EEEvNS_5KArgsE": (96, 0),
+    "_ZN4airs11rice_kernelILi0ELb0ELb1EEEvNS_5KArgsE": (96, 0),
     # encode_kernel<2, DIFF, ZERO, Rice, no model, FULL>: frames the Rice
     # kernel does not take (k > 7, holes in device-planned launch lists); no
     # longer a bench path, so the kernel-argument padding that kept it at 13
