@@ -493,7 +493,7 @@ __device__ __forceinline__ uint32_t rice_tail_wait(const KArgs &a, uint32_t gseg
 // reads the frame's spf * 16 granules (the frame barrier), takes the k with
 // the fewest bits n (k + 1) + S_k (ties to the smaller k) and the sum of
 // S_k over the segments before this one.  Leaves the arena zero again.
-__device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const uint32_t (&mp)[RCH][8], uint32_t gseg, uint32_t sif,
+__device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, uint32_t (&mp)[RCH][8], uint32_t gseg, uint32_t sif,
 			     uint32_t tid, uint32_t lane, uint32_t wid)
 {
 	__shared__ uint32_t s_hist[AUTO_BINS];
@@ -510,10 +510,10 @@ __device__ __forceinline__ uint2 rice_auto_k(const KArgs &a, uint32_t *H, const 
 	for (uint32_t c = 0; c < RCH; c++) {
 #pragma unroll
 		for (uint32_t jp = 0; jp < 8u; jp++) {
-			// an opaque copy of the pair: otherwise the compiler computes all
-			// 64 bins ahead of the barrier above
-			uint32_t wv = mp[c][jp];
-			asm volatile("" : "+v"(wv));
+			// the pair made opaque in place (no copy): otherwise the compiler
+			// computes all 64 bins ahead of the barrier above
+			asm volatile("" : "+v"(mp[c][jp]));
+			const uint32_t wv = mp[c][jp];
 #pragma unroll
 			for (uint32_t h = 0; h < 2; h++) {
 				const uint32_t v = (h ? wv >> 16 : wv & 0xFFFFu) + 1u;
